@@ -1,0 +1,89 @@
+"""Build libfa_hip.so in-tree for gfx950 with hipcc (no cmake, no torch extension machinery).
+
+    python hazyresearch_flash-attention_amd/build.py [--jobs N] [--force]
+
+Each head-dim tile is its own translation unit so the template instantiations compile in
+parallel. The shared object lands next to the Python package (flash_attn/libfa_hip.so), which
+is where flash_attn/flash_attn_hip.py loads it from.
+"""
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+BUILD = os.path.join(HERE, "build")
+OUT = os.path.join(HERE, "flash_attn", "libfa_hip.so")
+
+SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_d32.hip", "fa_d64.hip", "fa_d128.hip"]
+ARCH = os.environ.get("FA_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def common_flags():
+    return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
+            "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def _deps():
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hdrs.append(os.path.join(INCLUDE, "fa_hip.h"))
+    return hdrs + [os.path.abspath(__file__)]
+
+
+def compile_one(src, force=False, extra=()):
+    os.makedirs(BUILD, exist_ok=True)
+    obj = os.path.join(BUILD, src + ".o")
+    srcp = os.path.join(CSRC, src)
+    if not force and _newer(obj, [srcp] + _deps()):
+        return obj
+    lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
+    cmd = [hipcc()] + common_flags() + list(extra) + lang + ["-c", srcp, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(jobs=None, force=False, verbose=True):
+    jobs = jobs or min(len(SOURCES), os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: compile_one(s, force), SOURCES))
+    if not force and _newer(OUT, objs):
+        return OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"built {OUT}")
+    return OUT
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--force", action="store_true")
+    args = ap.parse_args()
+    try:
+        build(args.jobs, args.force)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

@@ -1,0 +1,143 @@
+// fa_api.cpp — the C ABI of libfa_hip.so (declared in include/fa_hip.h).
+//
+// Replaces the reference's pybind11 host layer (csrc/flash_attn/fmha_api.cpp:112-247):
+// argument validation (fmha_api.cpp:131-170, same rules, reported as error codes instead of
+// TORCH_CHECK/exit(1)), head-dim tile selection (fmha_fprop_kernel_dispatch.cu:90-134, here
+// 32/64/128 tiles instead of CUTLASS traits), and the launches. Dropout seed/offset arrive
+// from the caller (the Python layer reserves them from the torch generator), so the library
+// holds no generator state.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "fa_launch.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(FA_ERR_LAUNCH, "%s: HIP error %d (%s)", what, (int)e, hipGetErrorString(e));
+}
+
+int pick_tile(int head_dim) {
+    if (head_dim <= 32) return 32;
+    if (head_dim <= 64) return 64;
+    return 128;
+}
+
+template <typename Args>
+int check_common(const Args *a, const char *fn) {
+    if (a == nullptr) return fail(FA_ERR_INVALID_ARGUMENT, "%s: args is NULL", fn);
+    if (a->dtype != FA_DTYPE_FP16 && a->dtype != FA_DTYPE_BF16)
+        return fail(FA_ERR_INVALID_ARGUMENT, "%s: dtype must be fp16 or bf16", fn);
+    if (a->batch <= 0) return fail(FA_ERR_INVALID_ARGUMENT, "%s: batch_size must be > 0", fn);
+    if (a->nheads <= 0) return fail(FA_ERR_INVALID_ARGUMENT, "%s: num_heads must be > 0", fn);
+    if (a->head_dim <= 0 || a->head_dim % 8 != 0 || a->head_dim > 128)
+        return fail(FA_ERR_UNSUPPORTED, "%s: head_size must be a multiple of 8 and <= 128 (got %d)", fn,
+                    a->head_dim);
+    if (a->max_seqlen_q < 0 || a->max_seqlen_k < 0)
+        return fail(FA_ERR_INVALID_ARGUMENT, "%s: max_seqlen must be >= 0", fn);
+    if (!(a->p_dropout >= 0.f && a->p_dropout < 1.f))
+        return fail(FA_ERR_INVALID_ARGUMENT, "%s: p_dropout must be in [0, 1)", fn);
+    if (!std::isfinite(a->softmax_scale)) return fail(FA_ERR_INVALID_ARGUMENT, "%s: softmax_scale must be finite", fn);
+    if (a->lse_stride < a->max_seqlen_q) return fail(FA_ERR_INVALID_ARGUMENT, "%s: lse_stride < max_seqlen_q", fn);
+    if (!a->q || !a->k || !a->v || !a->softmax_lse || !a->cu_seqlens_q || !a->cu_seqlens_k)
+        return fail(FA_ERR_INVALID_ARGUMENT, "%s: NULL tensor pointer", fn);
+    return FA_OK;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+const char *fa_last_error(void) { return g_last_error.c_str(); }
+
+const char *fa_version(void) { return "fa_hip 0.1.0 (gfx950)"; }
+
+int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {
+    switch (what) {
+        case FA_QUERY_BWD_WORKSPACE: return a * b * c * (int64_t)sizeof(float);
+        case FA_QUERY_MAX_HEAD_DIM: return 128;
+        case FA_QUERY_RNG_INCREMENT: return 4;
+        case FA_QUERY_FWD_ARGS_SIZE: return (int64_t)sizeof(FaFwdArgs);
+        case FA_QUERY_BWD_ARGS_SIZE: return (int64_t)sizeof(FaBwdArgs);
+        default: return -1;
+    }
+}
+
+int fa_fwd(const FaFwdArgs *a, void *stream) {
+    g_last_error.clear();
+    int rc = check_common(a, "fa_fwd");
+    if (rc) return rc;
+    if (!a->o) return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: o is NULL");
+    if (!aligned16(a->q) || !aligned16(a->k) || !aligned16(a->v) || !aligned16(a->o) ||
+        (a->q_row_stride | a->k_row_stride | a->v_row_stride | a->o_row_stride | a->q_head_stride |
+         a->k_head_stride | a->v_head_stride | a->o_head_stride) % 8 != 0)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: q/k/v/o must be 16-byte aligned with strides multiple of 8");
+    if (a->s_dmask && (a->s_rows < a->max_seqlen_q || a->s_cols < a->max_seqlen_k))
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: s_dmask extents smaller than max_seqlen");
+    if (a->max_seqlen_q == 0) return FA_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    switch (pick_tile(a->head_dim)) {
+        case 32: e = fa::launch_fwd<32>(*a, s); break;
+        case 64: e = fa::launch_fwd<64>(*a, s); break;
+        default: e = fa::launch_fwd<128>(*a, s); break;
+    }
+    if (e != hipSuccess) return hip_fail(e, "fa_fwd launch");
+    if (a->s_dmask) {
+        e = fa::launch_probs(*a, s);
+        if (e != hipSuccess) return hip_fail(e, "fa_fwd probs launch");
+    }
+    return FA_OK;
+}
+
+int fa_bwd(const FaBwdArgs *a, void *stream) {
+    g_last_error.clear();
+    int rc = check_common(a, "fa_bwd");
+    if (rc) return rc;
+    if (!a->dout || !a->out || !a->dq || !a->dk || !a->dv || !a->softmax_d || !a->dq_accum)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: NULL tensor pointer");
+    if (!aligned16(a->q) || !aligned16(a->k) || !aligned16(a->v) || !aligned16(a->dout) || !aligned16(a->out) ||
+        !aligned16(a->dq) || !aligned16(a->dk) || !aligned16(a->dv) || !aligned16(a->dq_accum) ||
+        (a->q_row_stride | a->k_row_stride | a->v_row_stride | a->o_row_stride | a->do_row_stride |
+         a->dq_row_stride | a->dk_row_stride | a->dv_row_stride | a->q_head_stride | a->k_head_stride |
+         a->v_head_stride | a->o_head_stride | a->do_head_stride | a->dq_head_stride | a->dk_head_stride |
+         a->dv_head_stride) % 8 != 0)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: tensors must be 16-byte aligned with strides multiple of 8");
+    if (a->total_q < 0) return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: total_q < 0");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = fa::launch_bwd_pre(*a, s);
+    if (e != hipSuccess) return hip_fail(e, "fa_bwd pre launch");
+    if (a->max_seqlen_k > 0) {
+        switch (pick_tile(a->head_dim)) {
+            case 32: e = fa::launch_bwd<32>(*a, s); break;
+            case 64: e = fa::launch_bwd<64>(*a, s); break;
+            default: e = fa::launch_bwd<128>(*a, s); break;
+        }
+        if (e != hipSuccess) return hip_fail(e, "fa_bwd launch");
+    }
+    e = fa::launch_bwd_post(*a, s);
+    if (e != hipSuccess) return hip_fail(e, "fa_bwd post launch");
+    return FA_OK;
+}
+
+}  // extern "C"

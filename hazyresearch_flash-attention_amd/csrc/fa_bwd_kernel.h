@@ -1,0 +1,411 @@
+// fa_bwd_kernel.h — FlashAttention backward for gfx950 (CDNA4), hand-written HIP.
+//
+// The reference branch has no native backward (flash_attn_cuda.bwd is called at
+// flash_attn/flash_attn_interface.py:31-33 but never bound, fmha_api.cpp:244-247). Its contract
+// is rebuilt from that call signature and from autograd of attention_ref
+// (tests/test_flash_attn.py:115-159): with P = softmax(scale*QK^T), M the dropout keep mask,
+// pk = 1 - p_drop, Pd = P*M/pk, O = Pd V:
+//     dV = Pd^T dO,  dZ = dO V^T,  delta = rowsum(dO*O),  dS = P * (dZ*M/pk - delta),
+//     dQ = scale * dS K,  dK = scale * dS^T Q.
+//
+// Structure (MI355X-first): grid = (key blocks of 128, H, B); a workgroup = 4 waves, one wave
+// owns 32 keys and keeps K, V (as MFMA B operands) and dK^T, dV^T accumulators in registers for
+// the whole kernel. It sweeps 32-row query tiles: Q and dO tiles are staged into swizzled LDS
+// images that serve both row reads (S = Q K^T, dZ = dO V^T) and transposed reads
+// (dV^T += dO^T Pd, dK^T += Q^T dS). Scores are computed with the key on the MFMA lane, so
+// P/dS accumulators are already the B operands of dV^T/dK^T. dS crosses LDS once (a [key][query]
+// image) for dQ = dS K, computed with 16x16x32 MFMAs so each of the 4 waves owns whole dQ tiles
+// summed over all 128 keys, then added with fp32 atomics into a workspace; a last kernel scales
+// and converts dQ into the (possibly strided) output.
+#pragma once
+
+#include "fa_common.h"
+#include "../../include/fa_hip.h"
+
+namespace fa {
+
+template <int D>
+struct BwdCfg {
+    static constexpr int NW = 4;
+    static constexpr int BKV = 32 * NW;     // keys per workgroup
+    static constexpr int BQ = 32;           // query rows per iteration
+    static constexpr int NC = D / 8;
+    static constexpr int K_IMG = BKV * D * 2;
+    static constexpr int Q_IMG = BQ * D * 2;
+    static constexpr int DS_IMG = BKV * BQ * 2;
+    static constexpr int OFF_K = 0;
+    static constexpr int OFF_Q = OFF_K + K_IMG;
+    static constexpr int OFF_DO = OFF_Q + Q_IMG;
+    static constexpr int OFF_DS = OFF_DO + Q_IMG;
+    static constexpr int OFF_LSE = OFF_DS + DS_IMG;
+    static constexpr int OFF_DELTA = OFF_LSE + BQ * 4;
+    static constexpr int LDS_BYTES = OFF_DELTA + BQ * 4;
+};
+
+// byte offset in the dS^T image ([key][query], 64-B rows) of query column q (multiple of 4) of
+// key row r. The 32-B half is flipped on rows with bit 3 set so that the dQ transposed reads
+// (two 4-row blocks 8 rows apart per half-wave) are bank-conflict free.
+__device__ __forceinline__ int ds_off(int r, int q) { return r * 64 + ((q * 2) ^ (((r >> 3) & 1) << 5)); }
+
+// delta = rowsum(dO * O) (softmax_d), and zero the fp32 dQ accumulator.
+template <typename T>
+__global__ __launch_bounds__(64) void fa_bwd_dot_kernel(const FaBwdArgs a) {
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int q_start = a.cu_seqlens_q[b];
+    const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
+    const int row = blockIdx.x * 64 + threadIdx.x;
+    if (row >= seqlen_q) return;
+    const uint16_t *dop = (const uint16_t *)a.dout + (int64_t)(q_start + row) * a.do_row_stride + (int64_t)h * a.do_head_stride;
+    const uint16_t *op = (const uint16_t *)a.out + (int64_t)(q_start + row) * a.o_row_stride + (int64_t)h * a.o_head_stride;
+    float *acc = a.dq_accum + ((int64_t)(q_start + row) * a.nheads + h) * a.head_dim;
+    float sum = 0.f;
+    for (int c = 0; c < a.head_dim; c += 8) {
+        u32x4 x = gload128(dop + c), y = gload128(op + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            sum += T::to_float(x[e] & 0xFFFF) * T::to_float(y[e] & 0xFFFF);
+            sum += T::to_float(x[e] >> 16) * T::to_float(y[e] >> 16);
+        }
+        f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4 *>(acc + c) = z;
+        *reinterpret_cast<f32x4 *>(acc + c + 4) = z;
+    }
+    a.softmax_d[(int64_t)(b * a.nheads + h) * a.lse_stride + row] = sum;
+}
+
+// dq = scale * dq_accum, converted to 16-bit into the (possibly strided) dq.
+template <typename T>
+__global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs a) {
+    const int64_t nchunk_row = a.head_dim / 8;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t total = (int64_t)a.total_q * a.nheads * nchunk_row;
+    if (idx >= total) return;
+    const int64_t c = idx % nchunk_row;
+    const int64_t rh = idx / nchunk_row;
+    const int64_t h = rh % a.nheads;
+    const int64_t row = rh / a.nheads;
+    const float *src = a.dq_accum + (row * a.nheads + h) * a.head_dim + c * 8;
+    f32x4 x0 = *reinterpret_cast<const f32x4 *>(src);
+    f32x4 x1 = *reinterpret_cast<const f32x4 *>(src + 4);
+    const float s = a.softmax_scale;
+    u32x4 w = {T::pack2(x0[0] * s, x0[1] * s), T::pack2(x0[2] * s, x0[3] * s),
+               T::pack2(x1[0] * s, x1[1] * s), T::pack2(x1[2] * s, x1[3] * s)};
+    gstore128((uint16_t *)a.dq + row * a.dq_row_stride + h * a.dq_head_stride + c * 8, w);
+}
+
+template <int D, typename T, bool CAUSAL, bool DROPOUT>
+__global__ __launch_bounds__(256) void fa_bwd_kernel(const FaBwdArgs a) {
+    using C = BwdCfg<D>;
+    using S = Swz<D>;
+    constexpr float LOG2E = 1.4426950408889634f;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *kimg = smem + C::OFF_K;
+    char *qimg = smem + C::OFF_Q;
+    char *doimg = smem + C::OFF_DO;
+    char *dsimg = smem + C::OFF_DS;
+    float *lse_s = (float *)(smem + C::OFF_LSE);
+    float *del_s = (float *)(smem + C::OFF_DELTA);
+
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int q_start = a.cu_seqlens_q[b];
+    const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
+    const int k_start = a.cu_seqlens_k[b];
+    const int seqlen_k = a.cu_seqlens_k[b + 1] - k_start;
+    const int k0 = blockIdx.x * C::BKV;
+    if (k0 >= seqlen_k) return;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l32 = lane & 31;
+    const int hi = lane >> 5;
+    const int kw = k0 + 32 * wave;
+    const int kvrow = kw + l32;
+    const int head_dim = a.head_dim;
+
+    const uint16_t *qp = (const uint16_t *)a.q + (int64_t)q_start * a.q_row_stride + (int64_t)h * a.q_head_stride;
+    const uint16_t *dop = (const uint16_t *)a.dout + (int64_t)q_start * a.do_row_stride + (int64_t)h * a.do_head_stride;
+    const uint16_t *kp = (const uint16_t *)a.k + (int64_t)k_start * a.k_row_stride + (int64_t)h * a.k_head_stride;
+    const uint16_t *vp = (const uint16_t *)a.v + (int64_t)k_start * a.v_row_stride + (int64_t)h * a.v_head_stride;
+    const float *lse_g = a.softmax_lse + (int64_t)(b * a.nheads + h) * a.lse_stride;
+    const float *del_g = a.softmax_d + (int64_t)(b * a.nheads + h) * a.lse_stride;
+    float *dqa = a.dq_accum + ((int64_t)q_start * a.nheads + h) * head_dim;
+    const int64_t dqa_row = (int64_t)a.nheads * head_dim;
+
+    // ---- stage the K block image (B operand of dQ = dS K, transposed reads)
+    for (int idx = tid; idx < C::BKV * C::NC; idx += 256) {
+        const int row = idx / C::NC, c = idx % C::NC;
+        const int kv = k0 + row;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (kv < seqlen_k && c * 8 < head_dim) v = gload128(kp + (int64_t)kv * a.k_row_stride + c * 8);
+        lds_write128(kimg, S::off(row, c), v);
+    }
+    // ---- K, V rows of this lane's key as B operands: B[k=d][col=key]
+    typename T::frag kf[D / 16], vf[D / 16];
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+        const int c = 2 * ks + hi;
+        u32x4 kv4 = {0u, 0u, 0u, 0u}, vv4 = {0u, 0u, 0u, 0u};
+        if (kvrow < seqlen_k && c * 8 < head_dim) {
+            kv4 = gload128(kp + (int64_t)kvrow * a.k_row_stride + c * 8);
+            vv4 = gload128(vp + (int64_t)kvrow * a.v_row_stride + c * 8);
+        }
+        kf[ks] = as_frag<T>(kv4);
+        vf[ks] = as_frag<T>(vv4);
+    }
+
+    f32x16 dv[D / 32], dk[D / 32];
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { dv[dt][r] = 0.f; dk[dt][r] = 0.f; }
+
+    const float c_log2 = a.softmax_scale * LOG2E;
+    const float rp = 1.0f / (1.0f - a.p_dropout);
+    const uint32_t keep_thr = (uint32_t)floorf((1.0f - a.p_dropout) * 65535.0f);
+    const uint32_t seed_lo = (uint32_t)a.rng_seed, seed_hi = (uint32_t)(a.rng_seed >> 32);
+    const uint32_t rng_ctr3 = (uint32_t)(a.rng_offset >> 2);
+    const uint32_t bh = (uint32_t)(b * a.nheads + h);
+
+    const int grp = (lane >> 4) & 1;   // 16-lane group within the half (32x32 tr reads)
+    const int qq = (lane & 15) >> 2;
+    const int pp = lane & 3;
+    const int g4 = lane >> 4;          // 16-lane group index 0..3 (16x16x32 operands)
+
+    const int q_begin = CAUSAL ? k0 : 0;   // rows q < k0 see no key of this block
+    const int nqt = seqlen_q > q_begin ? (seqlen_q - q_begin + C::BQ - 1) / C::BQ : 0;
+
+    for (int it = 0; it < nqt; ++it) {
+        const int q0 = q_begin + it * C::BQ;
+        // ---- stage Q, dO tiles, lse (pre-multiplied by log2 e) and delta
+        for (int idx = tid; idx < C::BQ * C::NC; idx += 256) {
+            const int row = idx / C::NC, c = idx % C::NC;
+            const int q = q0 + row;
+            u32x4 x = {0u, 0u, 0u, 0u}, y = {0u, 0u, 0u, 0u};
+            if (q < seqlen_q && c * 8 < head_dim) {
+                x = gload128(qp + (int64_t)q * a.q_row_stride + c * 8);
+                y = gload128(dop + (int64_t)q * a.do_row_stride + c * 8);
+            }
+            lds_write128(qimg, S::off(row, c), x);
+            lds_write128(doimg, S::off(row, c), y);
+        }
+        if (tid < C::BQ) {
+            const int q = q0 + tid;
+            lse_s[tid] = q < seqlen_q ? lse_g[q] * LOG2E : 0.f;
+            del_s[tid] = q < seqlen_q ? del_g[q] : 0.f;
+        }
+        __syncthreads();
+
+        const bool active = !CAUSAL || (q0 + C::BQ - 1 >= kw);
+        f32x16 ds;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ds[r] = 0.f;
+        if (active) {
+            // ---- S = Q K^T and dZ = dO V^T : lane = key, registers = query rows crow(r,hi)
+            f32x16 sacc, zacc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; zacc[r] = 0.f; }
+#pragma unroll
+            for (int ks = 0; ks < D / 16; ++ks) {
+                u32x4 qa = lds_read128(qimg, S::off(l32, 2 * ks + hi));
+                u32x4 da = lds_read128(doimg, S::off(l32, 2 * ks + hi));
+                sacc = T::mfma32(as_frag<T>(qa), kf[ks], sacc);
+                zacc = T::mfma32(as_frag<T>(da), vf[ks], zacc);
+            }
+            // row constants for rows crow(4g+e, hi) = 8g + 4hi + e (16-B aligned groups of 4)
+            f32x4 lse4[4], del4[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                lse4[g] = *reinterpret_cast<const f32x4 *>(lse_s + 8 * g + 4 * hi);
+                del4[g] = *reinterpret_cast<const f32x4 *>(del_s + 8 * g + 4 * hi);
+            }
+            const bool need_mask = (q0 + C::BQ > seqlen_q) || (k0 + C::BKV > seqlen_k) ||
+                                   (CAUSAL && q0 < kw + 31);
+            u32x4 rw[2];
+            if (DROPOUT) {
+#pragma unroll
+                for (int sg = 0; sg < 2; ++sg) {
+                    const uint32_t g = ((uint32_t)(q0 >> 5) << 2) | (sg << 1) | hi;
+                    rw[sg] = philox7(g, (uint32_t)kvrow, bh, rng_ctr3, seed_lo, seed_hi);
+                }
+            }
+            f32x16 pd;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float lse2 = lse4[r >> 2][r & 3];
+                const float del = del4[r >> 2][r & 3];
+                float p = fast_exp2(fmaf(sacc[r], c_log2, -lse2));
+                if (need_mask) {
+                    const int q = q0 + crow(r, hi);
+                    if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
+                }
+                float dpv = zacc[r];
+                float pdv = p;
+                if (DROPOUT) {
+                    const int slot = (r & 3) | (((r >> 2) & 1) << 2);
+                    const uint32_t word = rw[r >> 3][slot >> 1];
+                    const uint32_t rnd = (slot & 1) ? (word >> 16) : (word & 0xFFFFu);
+                    const bool keep = rnd <= keep_thr;
+                    dpv = keep ? dpv * rp : 0.f;
+                    pdv = keep ? p * rp : 0.f;
+                }
+                pd[r] = pdv;
+                ds[r] = p * (dpv - del);
+            }
+            // ---- dV^T += dO^T Pd ; dK^T += Q^T dS  (A operands by transposed reads)
+#pragma unroll
+            for (int sg = 0; sg < 2; ++sg) {
+                u32x4 pk, sk;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    pk[e] = T::pack2(pd[8 * sg + 2 * e], pd[8 * sg + 2 * e + 1]);
+                    sk[e] = T::pack2(ds[8 * sg + 2 * e], ds[8 * sg + 2 * e + 1]);
+                }
+                const int rb = 16 * sg + 4 * hi + qq;
+#pragma unroll
+                for (int dt = 0; dt < D / 32; ++dt) {
+                    const int col = 32 * dt + 16 * grp + 4 * pp;
+                    u32x2 a0 = lds_read_tr(doimg, S::off8(rb, col));
+                    u32x2 a1 = lds_read_tr(doimg, S::off8(rb + 8, col));
+                    u32x4 av = {a0[0], a0[1], a1[0], a1[1]};
+                    dv[dt] = T::mfma32(as_frag<T>(av), as_frag<T>(pk), dv[dt]);
+                    u32x2 b0 = lds_read_tr(qimg, S::off8(rb, col));
+                    u32x2 b1 = lds_read_tr(qimg, S::off8(rb + 8, col));
+                    u32x4 bv = {b0[0], b0[1], b1[0], b1[1]};
+                    dk[dt] = T::mfma32(as_frag<T>(bv), as_frag<T>(sk), dk[dt]);
+                }
+            }
+        }
+        // ---- dS^T image: row = key (32*wave + l32), columns = query rows 8g + 4hi .. +3
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            u32x2 w = {T::pack2(ds[4 * g + 0], ds[4 * g + 1]), T::pack2(ds[4 * g + 2], ds[4 * g + 3])};
+            lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), w);
+        }
+        __syncthreads();
+
+        // ---- dQ[q][d] += dS[q][key] K[key][d] over the 128 keys (16x16x32 MFMAs)
+        {
+            const int qh = wave & 1;
+#pragma unroll
+            for (int t = 0; t < D / 32; ++t) {
+                const int dbase = 16 * ((wave >> 1) + 2 * t);
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                    const int r0 = 32 * ks + 8 * g4 + qq;
+                    u32x2 a0 = lds_read_tr(dsimg, ds_off(r0, 16 * qh + 4 * pp));
+                    u32x2 a1 = lds_read_tr(dsimg, ds_off(r0 + 4, 16 * qh + 4 * pp));
+                    u32x4 av = {a0[0], a0[1], a1[0], a1[1]};
+                    u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
+                    u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
+                    u32x4 bv = {b0[0], b0[1], b1[0], b1[1]};
+                    acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
+                }
+                const int d = dbase + (lane & 15);
+                if (d < head_dim) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int q = q0 + 16 * qh + 4 * g4 + i;
+                        if (q < seqlen_q) atomicAdd(dqa + (int64_t)q * dqa_row + d, acc[i]);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: dV, dK (scaled) rows of this lane's key
+    if (kvrow < seqlen_k) {
+        uint16_t *dvp = (uint16_t *)a.dv + (int64_t)(k_start + kvrow) * a.dv_row_stride + (int64_t)h * a.dv_head_stride;
+        uint16_t *dkp = (uint16_t *)a.dk + (int64_t)(k_start + kvrow) * a.dk_row_stride + (int64_t)h * a.dk_head_stride;
+        const float sc = a.softmax_scale;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = 32 * dt + 8 * g + 4 * hi;
+                if (d < head_dim) {
+                    u32x2 wv = {T::pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]),
+                                T::pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3])};
+                    u32x2 wk = {T::pack2(dk[dt][4 * g + 0] * sc, dk[dt][4 * g + 1] * sc),
+                                T::pack2(dk[dt][4 * g + 2] * sc, dk[dt][4 * g + 3] * sc)};
+                    gstore64(dvp + d, wv);
+                    gstore64(dkp + d, wk);
+                }
+            }
+    }
+}
+
+// Attention probabilities for return_attn_probs (test-only path, reference S_dmask
+// semantics of csrc/flash_attn/src/fmha/softmax.h:256-296 with this build's own layout):
+// s[b][h][row][col] = softmax(scale*QK^T)[row][col], negated where dropout dropped it,
+// 0 where masked or padded. Row-major (B, H, s_rows, s_cols).
+template <typename T, bool CAUSAL, bool DROPOUT>
+__global__ __launch_bounds__(256) void fa_probs_kernel(const FaFwdArgs a) {
+    // block = 32 query rows x 64 keys; thread = one key column x 8 rows (one Philox call)
+    constexpr float LOG2E = 1.4426950408889634f;
+    __shared__ float qs[32][129];
+    __shared__ float ks[64][129];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int q0 = blockIdx.x * 32;
+    const int q_start = a.cu_seqlens_q[b];
+    const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
+    const int k_start = a.cu_seqlens_k[b];
+    const int seqlen_k = a.cu_seqlens_k[b + 1] - k_start;
+    const int tid = threadIdx.x;
+    const int D = a.head_dim;
+    const uint16_t *qp = (const uint16_t *)a.q + (int64_t)q_start * a.q_row_stride + (int64_t)h * a.q_head_stride;
+    const uint16_t *kp = (const uint16_t *)a.k + (int64_t)k_start * a.k_row_stride + (int64_t)h * a.k_head_stride;
+    const float *lse_g = a.softmax_lse + (int64_t)(b * a.nheads + h) * a.lse_stride;
+    uint16_t *sp = (uint16_t *)a.s_dmask + (int64_t)(b * a.nheads + h) * a.s_rows * a.s_cols;
+    const float c_log2 = a.softmax_scale * LOG2E;
+    const uint32_t keep_thr = (uint32_t)floorf((1.0f - a.p_dropout) * 65535.0f);
+    const uint32_t bh = (uint32_t)(b * a.nheads + h);
+
+    for (int idx = tid; idx < 32 * D; idx += 256) {
+        const int r = idx / D, d = idx % D;
+        const int q = q0 + r;
+        qs[r][d] = q < seqlen_q ? T::to_float(qp[(int64_t)q * a.q_row_stride + d]) : 0.f;
+    }
+    const int col_l = tid & 63;
+    const int sg = (tid >> 6) & 1;
+    const int hh = tid >> 7;
+    for (int kv0 = 0; kv0 < a.s_cols; kv0 += 64) {
+        __syncthreads();
+        for (int idx = tid; idx < 64 * D; idx += 256) {
+            const int r = idx / D, d = idx % D;
+            const int kv = kv0 + r;
+            ks[r][d] = kv < seqlen_k ? T::to_float(kp[(int64_t)kv * a.k_row_stride + d]) : 0.f;
+        }
+        __syncthreads();
+        const int col = kv0 + col_l;
+        if (col >= a.s_cols) continue;
+        u32x4 w = {0u, 0u, 0u, 0u};
+        if (DROPOUT) {
+            const uint32_t g = ((uint32_t)(q0 >> 5) << 2) | (sg << 1) | hh;
+            w = philox7(g, (uint32_t)col, bh, (uint32_t)(a.rng_offset >> 2), (uint32_t)a.rng_seed,
+                        (uint32_t)(a.rng_seed >> 32));
+        }
+        for (int slot = 0; slot < 8; ++slot) {
+            const int r = 16 * sg + 4 * hh + (slot & 3) + 8 * (slot >> 2);
+            const int q = q0 + r;
+            if (q >= a.s_rows) continue;
+            float val = 0.f;
+            const bool valid = q < seqlen_q && col < seqlen_k && !(CAUSAL && col > q);
+            if (valid) {
+                float acc = 0.f;
+                for (int d = 0; d < D; ++d) acc = fmaf(qs[r][d], ks[col_l][d], acc);
+                val = fast_exp2(acc * c_log2 - lse_g[q] * LOG2E);
+                if (DROPOUT) {
+                    const uint32_t word = w[slot >> 1];
+                    const uint32_t rnd = (slot & 1) ? (word >> 16) : (word & 0xFFFFu);
+                    if (rnd > keep_thr) val = -val;
+                }
+            }
+            sp[(int64_t)q * a.s_cols + col] = T::from_float(val);
+        }
+    }
+}
+
+}  // namespace fa

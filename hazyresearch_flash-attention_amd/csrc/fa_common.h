@@ -1,0 +1,187 @@
+// fa_common.h — shared device helpers for the gfx950 FlashAttention kernels.
+//
+// Fragment maps used everywhere (cdna_hip_programming.md §3, v_mfma_f32_32x32x16_{bf16,f16}):
+//   lane l, r = l & 31, h = l >> 5
+//   A operand element j (0..7):  A[row r][k = 8h + j]
+//   B operand element j (0..7):  B[k = 8h + j][col r]
+//   C/D register i (0..15):      C[row crow(i, h)][col r],  crow(i,h) = (i&3) + 8(i>>2) + 4h
+// An accumulator X used as the B operand of k-step s takes registers 8s..8s+7 (converted to
+// 16-bit) and represents X rows 16s + 8(j>>2) + 4h + (j&3) — the other operand must supply
+// the same k order (what ds_read_b64_tr_b16 delivers below).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fa {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// 16-bit element traits: storage is raw 16-bit, MFMA operand type differs by dtype.
+struct Bf16 {
+    typedef bf16x8 frag;
+    static __device__ __forceinline__ uint16_t from_float(float x) {
+        __bf16 b = (__bf16)x;  // v_cvt_pk_bf16_f32, RNE, NaN-preserving
+        return __builtin_bit_cast(uint16_t, b);
+    }
+    static __device__ __forceinline__ float to_float(uint16_t x) {
+        return __uint_as_float(((uint32_t)x) << 16);
+    }
+    static __device__ __forceinline__ uint32_t pack2(float a, float b) {
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        bf16x2 v = {(__bf16)a, (__bf16)b};
+        return __builtin_bit_cast(uint32_t, v);
+    }
+    static __device__ __forceinline__ f32x16 mfma32(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ f32x4 mfma16(frag a, frag b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+};
+
+struct Fp16 {
+    typedef f16x8 frag;
+    static __device__ __forceinline__ uint16_t from_float(float x) {
+        _Float16 h = (_Float16)x;  // RNE
+        return __builtin_bit_cast(uint16_t, h);
+    }
+    static __device__ __forceinline__ float to_float(uint16_t x) {
+        return (float)__builtin_bit_cast(_Float16, x);
+    }
+    static __device__ __forceinline__ uint32_t pack2(float a, float b) {
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        f16x2 v = {(_Float16)a, (_Float16)b};
+        return __builtin_bit_cast(uint32_t, v);
+    }
+    static __device__ __forceinline__ f32x16 mfma32(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ f32x4 mfma16(frag a, frag b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+template <typename T>
+__device__ __forceinline__ typename T::frag as_frag(u32x4 v) {
+    return __builtin_bit_cast(typename T::frag, v);
+}
+
+__device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// ---------------------------------------------------------------------------------------
+// LDS tile image: [rows][D] 16-bit, 16-byte chunks XOR-swizzled so that
+//   (a) ds_read_b128 row reads (lane -> row r = l&31, fixed chunk) and
+//   (b) ds_read_b64_tr_b16 transposed reads (4 consecutive rows x 32 columns per half-wave)
+// are both bank-conflict free (derivation in DESIGN.md §4).
+// ---------------------------------------------------------------------------------------
+template <int D>
+struct Swz {
+    static constexpr int NC = D / 8;          // 16-B chunks per row
+    static constexpr int ROW_BYTES = D * 2;
+    static __device__ __forceinline__ int x(int r) {
+        if constexpr (D == 32) {
+            return (r >> 2) & 3;
+        } else if constexpr (D == 64) {
+            int u = (r >> 1) & 7;
+            return ((u & 1) << 2) | (u >> 1);
+        } else {  // 128
+            return ((r & 3) << 2) | ((r >> 2) & 3);
+        }
+    }
+    // byte offset of chunk c of row r
+    static __device__ __forceinline__ int off(int r, int c) { return r * ROW_BYTES + ((c ^ x(r)) << 4); }
+    // byte offset of the 8-byte half holding columns col..col+3 (col % 4 == 0) of row r
+    static __device__ __forceinline__ int off8(int r, int col) {
+        return off(r, col >> 3) + ((col >> 2) & 1) * 8;
+    }
+};
+
+__device__ __forceinline__ u32x4 lds_read128(const char *lds, int byte_off) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(
+        (const __attribute__((address_space(3))) char *)lds + byte_off);
+}
+__device__ __forceinline__ void lds_write128(char *lds, int byte_off, u32x4 v) {
+    *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(
+        (__attribute__((address_space(3))) char *)lds + byte_off) = v;
+}
+__device__ __forceinline__ void lds_write64(char *lds, int byte_off, u32x2 v) {
+    *reinterpret_cast<__attribute__((address_space(3))) u32x2 *>(
+        (__attribute__((address_space(3))) char *)lds + byte_off) = v;
+}
+// Transposed read: within each 16-lane group, lane 4q+p supplies the address of row q,
+// columns 4p..4p+3 of a 4x16 block; lane i of the group receives column i of the 4 rows.
+__device__ __forceinline__ u32x2 lds_read_tr(const char *lds, int byte_off) {
+    i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) i16x4 *)((__attribute__((address_space(3))) char *)lds + byte_off));
+    return __builtin_bit_cast(u32x2, v);
+}
+
+// Global 16-byte load / 8-byte store helpers.
+__device__ __forceinline__ u32x4 gload128(const void *p) { return *reinterpret_cast<const u32x4 *>(p); }
+__device__ __forceinline__ void gstore64(void *p, u32x2 v) { *reinterpret_cast<u32x2 *>(p) = v; }
+__device__ __forceinline__ void gstore128(void *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
+
+// Max over the lane pair (l, l^32) with v_permlane32_swap (T12).
+__device__ __forceinline__ float pair_max(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Dropout RNG: Philox-4x32 with 7 rounds (6 keyed rounds + final), the generator of the
+// reference (csrc/flash_attn/src/philox.cuh:30-59, 121-136), used as a pure counter-based
+// function of (seed, offset, bh, row, col) so forward and backward agree under any tiling:
+//
+//   g    = (row >> 5) << 2 | ((row >> 4) & 1) << 1 | ((row >> 2) & 1)
+//   slot = (row & 3) | ((row >> 3) & 1) << 2
+//   out  = Philox7(key = {seed_lo, seed_hi}, ctr = {g, col, bh, offset >> 2})
+//   rnd16(row, col) = 16-bit word `slot` of out (word slot>>1, low half first)
+//   keep(row, col)  = rnd16 <= floor((1 - p) * 65535)   (fmha_api.cpp:104, softmax.h:256-296)
+//
+// One Philox call serves the 8 rows {16s+4h+0..3, 16s+8+4h+0..3} of one column: exactly the
+// registers 8s..8s+7 of a 32x32 accumulator whose lane is the column (the backward's layout).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ u32x4 philox7(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                        uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    u32x4 r = {c0, c1, c2, c3};
+    return r;
+}
+
+__device__ __forceinline__ uint32_t rng_group(int row) {
+    return ((uint32_t)(row >> 5) << 2) | (((row >> 4) & 1) << 1) | ((row >> 2) & 1);
+}
+
+// Compare both 16-bit halves of w against thr; returns keep bits (bit0 = low half).
+__device__ __forceinline__ uint32_t keep2(uint32_t w, uint32_t thr) {
+    return ((w & 0xFFFFu) <= thr ? 1u : 0u) | ((w >> 16) <= thr ? 2u : 0u);
+}
+
+}  // namespace fa

@@ -1,0 +1,3 @@
+// Kernels for head-dim tile 32.
+#include "fa_kernels_impl.h"
+FA_INSTANTIATE(32)

@@ -1,0 +1,58 @@
+// fa_kernels_impl.h — template launchers; included by fa_d{32,64,128}.hip.
+#pragma once
+#include "fa_launch.h"
+#include "fa_fwd_kernel.h"
+#include "fa_bwd_kernel.h"
+
+namespace fa {
+
+template <int D, typename T, bool CAUSAL, bool DROPOUT>
+static hipError_t launch_fwd_t(const FaFwdArgs &a, hipStream_t stream) {
+    using C = FwdCfg<D>;
+    const int lds = C::lds_bytes(DROPOUT);
+    auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT>;
+    static const hipError_t attr_err =
+        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (attr_err != hipSuccess) return attr_err;
+    dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
+    return hipGetLastError();
+}
+
+template <int D, typename T, bool CAUSAL, bool DROPOUT>
+static hipError_t launch_bwd_t(const FaBwdArgs &a, hipStream_t stream) {
+    using C = BwdCfg<D>;
+    auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT>;
+    static const hipError_t attr_err =
+        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
+    if (attr_err != hipSuccess) return attr_err;
+    dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
+    hipLaunchKernelGGL(kern, grid, dim3(256), C::LDS_BYTES, stream, a);
+    return hipGetLastError();
+}
+
+template <int D, typename T>
+static hipError_t launch_fwd_dt(const FaFwdArgs &a, hipStream_t s) {
+    const bool dropout = a.p_dropout > 0.f;
+    if (a.is_causal) return dropout ? launch_fwd_t<D, T, true, true>(a, s) : launch_fwd_t<D, T, true, false>(a, s);
+    return dropout ? launch_fwd_t<D, T, false, true>(a, s) : launch_fwd_t<D, T, false, false>(a, s);
+}
+
+template <int D, typename T>
+static hipError_t launch_bwd_dt(const FaBwdArgs &a, hipStream_t s) {
+    const bool dropout = a.p_dropout > 0.f;
+    if (a.is_causal) return dropout ? launch_bwd_t<D, T, true, true>(a, s) : launch_bwd_t<D, T, true, false>(a, s);
+    return dropout ? launch_bwd_t<D, T, false, true>(a, s) : launch_bwd_t<D, T, false, false>(a, s);
+}
+
+}  // namespace fa
+
+#define FA_INSTANTIATE(D)                                                                        \
+    namespace fa {                                                                               \
+    template <> hipError_t launch_fwd<D>(const FaFwdArgs &a, hipStream_t s) {                    \
+        return a.dtype == FA_DTYPE_BF16 ? launch_fwd_dt<D, Bf16>(a, s) : launch_fwd_dt<D, Fp16>(a, s); \
+    }                                                                                            \
+    template <> hipError_t launch_bwd<D>(const FaBwdArgs &a, hipStream_t s) {                    \
+        return a.dtype == FA_DTYPE_BF16 ? launch_bwd_dt<D, Bf16>(a, s) : launch_bwd_dt<D, Fp16>(a, s); \
+    }                                                                                            \
+    }

@@ -1,0 +1,13 @@
+// fa_launch.h — host launchers for the gfx950 kernels (one translation unit per head-dim tile).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "../../include/fa_hip.h"
+
+namespace fa {
+// D is the padded head-dim tile (32, 64 or 128); the kernels zero-fill head_dim < D.
+template <int D> hipError_t launch_fwd(const FaFwdArgs &a, hipStream_t stream);
+template <int D> hipError_t launch_bwd(const FaBwdArgs &a, hipStream_t stream);
+hipError_t launch_probs(const FaFwdArgs &a, hipStream_t stream);
+hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t stream);
+hipError_t launch_bwd_post(const FaBwdArgs &a, hipStream_t stream);
+}  // namespace fa

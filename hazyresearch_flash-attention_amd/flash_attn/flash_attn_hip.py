@@ -1,0 +1,274 @@
+"""Host binding of libfa_hip.so — the MI355X replacement of the reference's `flash_attn_cuda`.
+
+`fwd` keeps the exact signature and return value of the reference's pybind11 `fwd`
+(csrc/flash_attn/fmha_api.cpp:112-125, 239-241): ``[out, softmax_lse, (S_dmask)]``, and `bwd`
+the signature the reference interface calls but never bound (flash_attn/flash_attn_interface.py:31-33),
+returning ``softmax_d``. Both accept one extra keyword, ``rng_state=(seed, offset)``, so that
+the autograd layer can replay a forward's dropout mask without saving the whole RNG state.
+
+The library is loaded with ctypes (plain C ABI, include/fa_hip.h). There is no CPU fallback:
+if the shared object is missing every call raises.
+"""
+import ctypes
+import math
+import os
+
+import torch
+
+_LIB_PATH = os.environ.get("FA_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfa_hip.so"))
+
+FA_DTYPE_FP16 = 0
+FA_DTYPE_BF16 = 1
+FA_QUERY_BWD_WORKSPACE = 1
+FA_QUERY_MAX_HEAD_DIM = 2
+FA_QUERY_RNG_INCREMENT = 3
+FA_QUERY_FWD_ARGS_SIZE = 4
+FA_QUERY_BWD_ARGS_SIZE = 5
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_u64 = ctypes.c_uint64
+_f32 = ctypes.c_float
+
+
+class FaFwdArgs(ctypes.Structure):
+    """ctypes mirror of FaFwdArgs (include/fa_hip.h)."""
+    _fields_ = [
+        ("q", _vp), ("k", _vp), ("v", _vp), ("o", _vp), ("softmax_lse", _vp), ("s_dmask", _vp),
+        ("cu_seqlens_q", _vp), ("cu_seqlens_k", _vp),
+        ("q_row_stride", _i64), ("q_head_stride", _i64),
+        ("k_row_stride", _i64), ("k_head_stride", _i64),
+        ("v_row_stride", _i64), ("v_head_stride", _i64),
+        ("o_row_stride", _i64), ("o_head_stride", _i64),
+        ("batch", _i32), ("nheads", _i32), ("head_dim", _i32),
+        ("max_seqlen_q", _i32), ("max_seqlen_k", _i32), ("lse_stride", _i32),
+        ("s_rows", _i32), ("s_cols", _i32),
+        ("softmax_scale", _f32), ("p_dropout", _f32),
+        ("rng_seed", _u64), ("rng_offset", _u64),
+        ("is_causal", _i32), ("dtype", _i32),
+    ]
+
+
+class FaBwdArgs(ctypes.Structure):
+    """ctypes mirror of FaBwdArgs (include/fa_hip.h)."""
+    _fields_ = [
+        ("dout", _vp), ("q", _vp), ("k", _vp), ("v", _vp), ("out", _vp), ("softmax_lse", _vp),
+        ("dq", _vp), ("dk", _vp), ("dv", _vp), ("softmax_d", _vp), ("dq_accum", _vp),
+        ("cu_seqlens_q", _vp), ("cu_seqlens_k", _vp),
+        ("do_row_stride", _i64), ("do_head_stride", _i64),
+        ("q_row_stride", _i64), ("q_head_stride", _i64),
+        ("k_row_stride", _i64), ("k_head_stride", _i64),
+        ("v_row_stride", _i64), ("v_head_stride", _i64),
+        ("o_row_stride", _i64), ("o_head_stride", _i64),
+        ("dq_row_stride", _i64), ("dq_head_stride", _i64),
+        ("dk_row_stride", _i64), ("dk_head_stride", _i64),
+        ("dv_row_stride", _i64), ("dv_head_stride", _i64),
+        ("batch", _i32), ("nheads", _i32), ("head_dim", _i32),
+        ("max_seqlen_q", _i32), ("max_seqlen_k", _i32),
+        ("total_q", _i32), ("lse_stride", _i32),
+        ("softmax_scale", _f32), ("p_dropout", _f32),
+        ("rng_seed", _u64), ("rng_offset", _u64),
+        ("is_causal", _i32), ("dtype", _i32),
+    ]
+
+
+_lib_handle = None
+
+
+def lib():
+    """Load libfa_hip.so (once). Raises if it is missing: there is no fallback path."""
+    global _lib_handle
+    if _lib_handle is None:
+        if not os.path.exists(_LIB_PATH):
+            raise ImportError(
+                f"libfa_hip.so not found at {_LIB_PATH}; build it with "
+                f"`python hazyresearch_flash-attention_amd/build.py`")
+        h = ctypes.CDLL(_LIB_PATH)
+        h.fa_fwd.argtypes = [ctypes.POINTER(FaFwdArgs), _vp]
+        h.fa_fwd.restype = ctypes.c_int
+        h.fa_bwd.argtypes = [ctypes.POINTER(FaBwdArgs), _vp]
+        h.fa_bwd.restype = ctypes.c_int
+        h.fa_query.argtypes = [ctypes.c_int, _i64, _i64, _i64]
+        h.fa_query.restype = _i64
+        h.fa_last_error.argtypes = []
+        h.fa_last_error.restype = ctypes.c_char_p
+        h.fa_version.argtypes = []
+        h.fa_version.restype = ctypes.c_char_p
+        if h.fa_query(FA_QUERY_FWD_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaFwdArgs):
+            raise ImportError("FaFwdArgs layout mismatch between fa_hip.h and flash_attn_hip.py")
+        if h.fa_query(FA_QUERY_BWD_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaBwdArgs):
+            raise ImportError("FaBwdArgs layout mismatch between fa_hip.h and flash_attn_hip.py")
+        _lib_handle = h
+    return _lib_handle
+
+
+def _check(cond, msg):
+    # TORCH_CHECK raises RuntimeError (fmha_api.cpp:131-170); keep that error type.
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _dtype_code(t):
+    if t == torch.float16:
+        return FA_DTYPE_FP16
+    if t == torch.bfloat16:
+        return FA_DTYPE_BF16
+    raise RuntimeError(f"FlashAttention only supports fp16 and bf16, got {t}")
+
+
+def _round16(x):
+    return (x + 15) // 16 * 16
+
+
+def _stream_ptr(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def reserve_rng(device, gen=None, increment=None):
+    """Reserve a Philox (seed, offset) pair from the torch generator, like
+    `gen->philox_cuda_state(counter_offset)` under the generator mutex (fmha_api.cpp:228-235)."""
+    if increment is None:
+        increment = 4
+    if gen is None:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        gen = torch.cuda.default_generators[idx]
+    seed = gen.initial_seed()
+    offset = gen.get_offset()
+    gen.set_offset(offset + increment)
+    return int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset)
+
+
+def _raise(rc, what):
+    msg = lib().fa_last_error().decode()
+    raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropout, softmax_scale,
+        zero_tensors, is_causal, return_softmax, gen, rng_state=None):
+    """Forward pass; same arguments and result as the reference's `flash_attn_cuda.fwd`."""
+    dt = _dtype_code(q.dtype)
+    _check(k.dtype == q.dtype and v.dtype == q.dtype, "q, k, v must have the same dtype")
+    _check(cu_seqlens_q.dtype == torch.int32 and cu_seqlens_k.dtype == torch.int32, "cu_seqlens must be int32")
+    _check(q.is_cuda and k.is_cuda and v.is_cuda and cu_seqlens_q.is_cuda and cu_seqlens_k.is_cuda,
+           "all tensors must be on the GPU")
+    _check(q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1, "last dimension must be contiguous")
+    _check(cu_seqlens_q.is_contiguous() and cu_seqlens_k.is_contiguous(), "cu_seqlens must be contiguous")
+    _check(q.dim() == 3 and k.dim() == 3 and v.dim() == 3, "q, k, v must be (total, nheads, headdim)")
+    batch = cu_seqlens_q.numel() - 1
+    total_q, nheads, head_dim = q.shape
+    total_k = k.shape[0]
+    _check(batch > 0, "batch_size must be positive")
+    _check(head_dim % 8 == 0 and head_dim <= 128, "head_size must be a multiple of 8 and <= 128")
+    _check(tuple(k.shape) == (total_k, nheads, head_dim) and tuple(v.shape) == (total_k, nheads, head_dim),
+           "k, v must have shape (total_k, nheads, headdim)")
+    _check(cu_seqlens_k.numel() == batch + 1, "cu_seqlens_k must have shape (batch_size + 1)")
+    _check(0.0 <= p_dropout < 1.0, "dropout_p must be in [0, 1)")
+    max_seqlen_q = int(max_seqlen_q)
+    max_seqlen_k = int(max_seqlen_k)
+    dev = q.device
+
+    with torch.cuda.device(dev):
+        o = torch.empty((total_q, nheads, head_dim), dtype=q.dtype, device=dev)
+        lse_stride = max(_round16(max_seqlen_q), 16)
+        lse = torch.empty((batch, nheads, lse_stride), dtype=torch.float32, device=dev)
+        s = None
+        if return_softmax:
+            s = torch.empty((batch, nheads, lse_stride, max(_round16(max_seqlen_k), 16)), dtype=q.dtype, device=dev)
+        if zero_tensors:
+            o.zero_()
+            lse.fill_(-math.inf)
+            if s is not None:
+                s.zero_()
+        if p_dropout > 0.0:
+            seed, offset = rng_state if rng_state is not None else reserve_rng(dev, gen)
+        else:
+            seed, offset = 0, 0
+        a = FaFwdArgs()
+        a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
+        a.softmax_lse = lse.data_ptr()
+        a.s_dmask = s.data_ptr() if s is not None else None
+        a.cu_seqlens_q, a.cu_seqlens_k = cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr()
+        a.q_row_stride, a.q_head_stride = q.stride(0), q.stride(1)
+        a.k_row_stride, a.k_head_stride = k.stride(0), k.stride(1)
+        a.v_row_stride, a.v_head_stride = v.stride(0), v.stride(1)
+        a.o_row_stride, a.o_head_stride = o.stride(0), o.stride(1)
+        a.batch, a.nheads, a.head_dim = batch, nheads, head_dim
+        a.max_seqlen_q, a.max_seqlen_k, a.lse_stride = max_seqlen_q, max_seqlen_k, lse_stride
+        if s is not None:
+            a.s_rows, a.s_cols = s.shape[2], s.shape[3]
+        a.softmax_scale = float(softmax_scale)
+        a.p_dropout = float(p_dropout)
+        a.rng_seed, a.rng_offset = seed, offset
+        a.is_causal = 1 if is_causal else 0
+        a.dtype = dt
+        rc = lib().fa_fwd(ctypes.byref(a), _stream_ptr(dev))
+        if rc != 0:
+            _raise(rc, "fa_fwd")
+    result = [o, lse]
+    if return_softmax:
+        result.append(s)
+    return result
+
+
+def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
+        p_dropout, softmax_scale, zero_tensors, is_causal, gen, rng_state=None):
+    """Backward pass with the signature flash_attn_interface.py:31-33 expects. Writes dq, dk, dv
+    in place (strided views allowed) and returns softmax_d = rowsum(dout * out), (B, H, lse_stride)."""
+    dt = _dtype_code(q.dtype)
+    for t, n in ((dout, "dout"), (k, "k"), (v, "v"), (out, "out"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
+        _check(t.dtype == q.dtype, f"{n} must have the dtype of q")
+        _check(t.is_cuda, f"{n} must be on the GPU")
+    if dout.stride(-1) != 1:
+        dout = dout.contiguous()
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
+        _check(t.stride(-1) == 1, f"{n} must have contiguous last dimension")
+    _check(softmax_lse.dtype == torch.float32 and softmax_lse.is_contiguous(), "softmax_lse must be fp32 contiguous")
+    batch = cu_seqlens_q.numel() - 1
+    total_q, nheads, head_dim = q.shape
+    _check(head_dim % 8 == 0 and head_dim <= 128, "head_size must be a multiple of 8 and <= 128")
+    _check(tuple(dq.shape) == tuple(q.shape) and tuple(dout.shape) == tuple(q.shape) and tuple(out.shape) == tuple(q.shape),
+           "dq/dout/out must have the shape of q")
+    _check(tuple(dk.shape) == tuple(k.shape) and tuple(dv.shape) == tuple(v.shape), "dk/dv must match k/v")
+    lse_stride = softmax_lse.shape[-1]
+    dev = q.device
+    with torch.cuda.device(dev):
+        if zero_tensors:
+            dq.zero_()
+            dk.zero_()
+            dv.zero_()
+        softmax_d = torch.empty((batch, nheads, lse_stride), dtype=torch.float32, device=dev)
+        dq_accum = torch.empty((total_q, nheads, head_dim), dtype=torch.float32, device=dev)
+        if p_dropout > 0.0:
+            # Without rng_state, draw from the generator like the reference protocol does: the
+            # caller restored the forward's RNG state (flash_attn_interface.py:60-63), so the
+            # same (seed, offset) comes out again.
+            seed, offset = rng_state if rng_state is not None else reserve_rng(dev, gen)
+        else:
+            seed, offset = 0, 0
+        a = FaBwdArgs()
+        a.dout, a.q, a.k, a.v, a.out = dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
+        a.softmax_lse = softmax_lse.data_ptr()
+        a.dq, a.dk, a.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+        a.softmax_d, a.dq_accum = softmax_d.data_ptr(), dq_accum.data_ptr()
+        a.cu_seqlens_q, a.cu_seqlens_k = cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr()
+        a.do_row_stride, a.do_head_stride = dout.stride(0), dout.stride(1)
+        a.q_row_stride, a.q_head_stride = q.stride(0), q.stride(1)
+        a.k_row_stride, a.k_head_stride = k.stride(0), k.stride(1)
+        a.v_row_stride, a.v_head_stride = v.stride(0), v.stride(1)
+        a.o_row_stride, a.o_head_stride = out.stride(0), out.stride(1)
+        a.dq_row_stride, a.dq_head_stride = dq.stride(0), dq.stride(1)
+        a.dk_row_stride, a.dk_head_stride = dk.stride(0), dk.stride(1)
+        a.dv_row_stride, a.dv_head_stride = dv.stride(0), dv.stride(1)
+        a.batch, a.nheads, a.head_dim = batch, nheads, head_dim
+        a.max_seqlen_q, a.max_seqlen_k = int(max_seqlen_q), int(max_seqlen_k)
+        a.total_q, a.lse_stride = total_q, lse_stride
+        a.softmax_scale = float(softmax_scale)
+        a.p_dropout = float(p_dropout)
+        a.rng_seed, a.rng_offset = seed, offset
+        a.is_causal = 1 if is_causal else 0
+        a.dtype = dt
+        rc = lib().fa_bwd(ctypes.byref(a), _stream_ptr(dev))
+        if rc != 0:
+            _raise(rc, "fa_bwd")
+    return softmax_d

@@ -1,0 +1,139 @@
+/*
+ * fa_hip.h — C ABI of libfa_hip.so, the MI355X (gfx950) FlashAttention library.
+ *
+ * This is the drop-in boundary for the reference's pybind11 module `flash_attn_cuda`
+ * (reference: setup.py:117-121). Each entry point replaces one reference interface:
+ *
+ *   fa_fwd  <- flash_attn_cuda.fwd  = mha_fwd   (csrc/flash_attn/fmha_api.cpp:112-242,
+ *                                                  bound at fmha_api.cpp:244-247)
+ *   fa_bwd  <- flash_attn_cuda.bwd              (called at flash_attn/flash_attn_interface.py:31-33;
+ *                                                  never bound in the reference, built fresh here)
+ *   fa_query, fa_last_error, fa_version: host helpers (no reference counterpart; the reference
+ *                                                  raised through TORCH_CHECK / exit(1),
+ *                                                  fmha_api.cpp:131-170, fmha_utils.h:36-48)
+ *
+ * Conventions:
+ *   - Plain C types only: raw device pointers, element strides (int64), sizes. No torch types.
+ *   - The caller allocates every output and workspace (the Python layer uses torch.empty).
+ *   - Every call is stream-ordered and asynchronous on `stream` (a hipStream_t, NULL = default).
+ *     No host synchronisation, no allocation, no exit(); safe for hipGraph capture.
+ *   - Return 0 on success; non-zero = error, with a message in fa_last_error() (thread-local).
+ *   - No global mutable state: concurrent calls from several host threads are safe.
+ *
+ * Layout ("unpadded", reference fmha_api.cpp:113-115,149-151): q is (total_q, H, D), k/v are
+ * (total_k, H, D), with stride(-1) == 1 and arbitrary row/head strides (packed qkv/kv views).
+ * Sequences are delimited by int32 cu_seqlens (B+1) on the device.
+ */
+#ifndef FA_HIP_H_
+#define FA_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { FA_DTYPE_FP16 = 0, FA_DTYPE_BF16 = 1 };
+
+/* Error codes. */
+enum {
+    FA_OK = 0,
+    FA_ERR_INVALID_ARGUMENT = 1,
+    FA_ERR_UNSUPPORTED = 2,
+    FA_ERR_LAUNCH = 3,
+};
+
+/* Forward arguments. Mirrors mha_fwd's parameters (fmha_api.cpp:112-125) plus the
+ * pointers/strides that set_params_fprop fills (fmha_api.cpp:38-110). */
+typedef struct FaFwdArgs {
+    const void *q;            /* (total_q, H, D) fp16/bf16 */
+    const void *k;            /* (total_k, H, D) */
+    const void *v;            /* (total_k, H, D) */
+    void *o;                  /* (total_q, H, D) output, same dtype */
+    float *softmax_lse;       /* (B, H, lse_stride) fp32 output; natural-log LSE of scaled scores */
+    void *s_dmask;            /* optional (B, H, s_rows, s_cols) probabilities, dtype of q; NULL = off */
+    const int32_t *cu_seqlens_q;  /* (B+1) device */
+    const int32_t *cu_seqlens_k;  /* (B+1) device */
+    int64_t q_row_stride, q_head_stride;   /* element strides */
+    int64_t k_row_stride, k_head_stride;
+    int64_t v_row_stride, v_head_stride;
+    int64_t o_row_stride, o_head_stride;
+    int32_t batch;            /* B */
+    int32_t nheads;           /* H */
+    int32_t head_dim;         /* D: multiple of 8, <= 128 (fmha_api.cpp:158) */
+    int32_t max_seqlen_q;
+    int32_t max_seqlen_k;
+    int32_t lse_stride;       /* >= max_seqlen_q (the Python layer uses round16(max_seqlen_q)) */
+    int32_t s_rows, s_cols;   /* s_dmask extents (>= max_seqlen_q, >= max_seqlen_k) */
+    float softmax_scale;
+    float p_dropout;          /* probability of DROPPING, in [0, 1) (fmha_api.cpp:99-107) */
+    uint64_t rng_seed;        /* Philox key */
+    uint64_t rng_offset;      /* Philox stream offset reserved from the torch generator */
+    int32_t is_causal;        /* top-left aligned: col <= row (mask.h:58-72) */
+    int32_t dtype;            /* FA_DTYPE_* */
+} FaFwdArgs;
+
+/* Backward arguments. Mirrors the bwd call made by flash_attn_interface.py:31-33:
+ * bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_q, cu_k, max_q, max_k, p, scale,
+ *     zero_tensors, causal, gen) -> softmax_d. */
+typedef struct FaBwdArgs {
+    const void *dout;         /* (total_q, H, D) */
+    const void *q;
+    const void *k;
+    const void *v;
+    const void *out;          /* forward output */
+    const float *softmax_lse; /* (B, H, lse_stride) from fa_fwd */
+    void *dq;                 /* (total_q, H, D) output; may be a strided view (qkv-packed) */
+    void *dk;                 /* (total_k, H, D) output; may be a strided view */
+    void *dv;
+    float *softmax_d;         /* (B, H, lse_stride) fp32 output: rowsum(dout * out) */
+    float *dq_accum;          /* workspace: fa_query(FA_QUERY_BWD_WORKSPACE) bytes, any contents */
+    const int32_t *cu_seqlens_q;
+    const int32_t *cu_seqlens_k;
+    int64_t do_row_stride, do_head_stride;
+    int64_t q_row_stride, q_head_stride;
+    int64_t k_row_stride, k_head_stride;
+    int64_t v_row_stride, v_head_stride;
+    int64_t o_row_stride, o_head_stride;
+    int64_t dq_row_stride, dq_head_stride;
+    int64_t dk_row_stride, dk_head_stride;
+    int64_t dv_row_stride, dv_head_stride;
+    int32_t batch, nheads, head_dim, max_seqlen_q, max_seqlen_k;
+    int32_t total_q;          /* rows of q / dq */
+    int32_t lse_stride;
+    float softmax_scale;
+    float p_dropout;
+    uint64_t rng_seed;        /* must equal the forward's seed/offset to replay its dropout mask */
+    uint64_t rng_offset;
+    int32_t is_causal;
+    int32_t dtype;
+} FaBwdArgs;
+
+/* Forward pass. Writes o, softmax_lse and (if s_dmask != NULL) the attention probabilities
+ * softmax(QK^T*scale) in row-major (B, H, s_rows, s_cols), with dropped entries negated
+ * (the sign convention of the reference, softmax.h:256-296). */
+int fa_fwd(const FaFwdArgs *args, void *stream);
+
+/* Backward pass. Writes dq, dk, dv and softmax_d. */
+int fa_bwd(const FaBwdArgs *args, void *stream);
+
+enum {
+    FA_QUERY_BWD_WORKSPACE = 1,   /* a = total_q, b = nheads, c = head_dim -> bytes */
+    FA_QUERY_MAX_HEAD_DIM = 2,    /* -> 128 */
+    FA_QUERY_RNG_INCREMENT = 3,   /* Philox offset increment a forward reserves per call */
+    FA_QUERY_FWD_ARGS_SIZE = 4,   /* sizeof(FaFwdArgs): lets FFI bindings check their struct layout */
+    FA_QUERY_BWD_ARGS_SIZE = 5,   /* sizeof(FaBwdArgs) */
+};
+int64_t fa_query(int what, int64_t a, int64_t b, int64_t c);
+
+/* Last error message of the calling host thread ("" if none). */
+const char *fa_last_error(void);
+
+/* Library version string. */
+const char *fa_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FA_HIP_H_ */

@@ -1,0 +1,100 @@
+"""Restatement of the reference's correctness oracle and test-input helpers.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Follows /root/reference/tests/test_flash_attn.py:
+  generate_random_padding_mask  :17-26
+  generate_qkv                  :29-112  (inputs built directly, no nn.Linear)
+  attention_ref                 :115-159 (fp32 upcast oracle; upcast=False + reorder_ops is the
+                                          "PyTorch baseline error" estimator of the 2x rule :407-409)
+  get_dropout_fraction          :300-329
+The reference's attention_ref raises UnboundLocalError when dropout_mask is None (:153-155);
+here a missing mask means "keep everything".
+"""
+import math
+
+import torch
+
+
+def generate_random_padding_mask(max_seqlen, batch_size, device, mode="random", generator=None):
+    assert mode in ("full", "random", "third")
+    if mode == "full":
+        lengths = torch.full((batch_size, 1), max_seqlen, device=device, dtype=torch.int32)
+    elif mode == "random":
+        lengths = torch.randint(max(1, max_seqlen - 20), max_seqlen, (batch_size, 1), device=device,
+                                generator=generator)
+    else:
+        lengths = torch.randint(max_seqlen // 3, max_seqlen, (batch_size, 1), device=device, generator=generator)
+    return torch.arange(max_seqlen, device=device)[None, :] < lengths
+
+
+def unpad(x, mask):
+    """x (B, S, ...) + mask (B, S) -> (x_unpad (total, ...), indices, cu_seqlens int32, max_seqlen)."""
+    seqlens = mask.sum(dim=-1, dtype=torch.int32)
+    indices = torch.nonzero(mask.reshape(-1), as_tuple=False).reshape(-1)
+    cu = torch.zeros(mask.shape[0] + 1, dtype=torch.int32, device=mask.device)
+    cu[1:] = torch.cumsum(seqlens, 0)
+    flat = x.reshape((-1,) + tuple(x.shape[2:]))
+    return flat.index_select(0, indices), indices, cu, int(seqlens.max().item())
+
+
+def pad(x_unpad, indices, batch, seqlen):
+    out = x_unpad.new_zeros((batch * seqlen,) + tuple(x_unpad.shape[1:]))
+    out.index_copy_(0, indices, x_unpad)
+    return out.reshape((batch, seqlen) + tuple(x_unpad.shape[1:]))
+
+
+def attention_ref(q, k, v, query_padding_mask=None, key_padding_mask=None, dropout_p=0.0,
+                  dropout_mask=None, causal=False, upcast=True, reorder_ops=False):
+    """q (B, Sq, H, D), k/v (B, Sk, H, D); masks (B, S) bool (True = valid);
+    dropout_mask (B, H, Sq, Sk) bool (True = keep). Returns (output (B,Sq,H,D), attention (B,H,Sq,Sk))."""
+    dtype_og = q.dtype
+    if upcast:
+        q, k, v = q.float(), k.float(), v.float()
+    seqlen_q, seqlen_k = q.shape[1], k.shape[1]
+    d = q.shape[-1]
+    if not reorder_ops:
+        scores = torch.einsum("bthd,bshd->bhts", q / math.sqrt(d), k)
+    else:
+        scores = torch.einsum("bthd,bshd->bhts", q, k / math.sqrt(d))
+    if key_padding_mask is not None:
+        scores.masked_fill_(~key_padding_mask[:, None, None, :], float("-inf"))
+    if causal:
+        cm = torch.triu(torch.ones(seqlen_q, seqlen_k, dtype=torch.bool, device=q.device), 1)
+        scores.masked_fill_(cm, float("-inf"))
+    attention = torch.softmax(scores, dim=-1)
+    dropout_scaling = 1.0 / (1 - dropout_p)
+    attention_drop = attention if dropout_mask is None else attention.masked_fill(~dropout_mask, 0.0)
+    output = torch.einsum("bhts,bshd->bthd", attention_drop, v * dropout_scaling)
+    if query_padding_mask is not None:
+        output.masked_fill_(~query_padding_mask[:, :, None, None], 0.0)
+        attention = attention.masked_fill(~query_padding_mask[:, None, :, None], 0.0)
+    return output.to(dtype=dtype_og), attention.to(dtype=dtype_og)
+
+
+def get_dropout_fraction(dropout_mask, query_padding_mask=None, key_padding_mask=None, causal=False):
+    batch_size, nheads, seqlen_q, seqlen_k = dropout_mask.shape
+    dropped = ~dropout_mask
+    if query_padding_mask is not None:
+        dropped = dropped.masked_fill(~query_padding_mask[:, None, :, None], False)
+    if key_padding_mask is not None:
+        dropped = dropped.masked_fill(~key_padding_mask[:, None, None, :], False)
+    if causal:
+        cm = torch.triu(torch.ones(seqlen_q, seqlen_k, dtype=torch.bool, device=dropout_mask.device), 1)
+        dropped = dropped.masked_fill(cm, False)
+    dropped_total = dropped.sum()
+    ql = (query_padding_mask.sum(dim=-1) if query_padding_mask is not None
+          else torch.full((batch_size,), seqlen_q, device=dropout_mask.device))
+    kl = (key_padding_mask.sum(dim=-1) if key_padding_mask is not None
+          else torch.full((batch_size,), seqlen_k, device=dropout_mask.device))
+    if not causal:
+        numel = ql * kl
+    else:
+        numel = torch.where(ql <= kl, ql * (ql + 1) / 2, ql * kl - (kl * (kl - 1) / 2))
+    return dropped_total / (numel.sum() * nheads)
+
+
+def max_err_bound(out_pt, out_ref, floor=0.0):
+    """The reference's 2x rule (tests/test_flash_attn.py:407-409): allowed max |out - ref|.
+    `floor` covers fp32 inputs, where the PyTorch baseline error can be exactly 0."""
+    return max(2 * (out_pt.float() - out_ref.float()).abs().max().item(), floor)
