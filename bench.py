@@ -1,0 +1,221 @@
+"""Benchmark: attention forward TFLOPS (and % of MI355X bf16 MFMA peak) at S=2048, D=64.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-extra] [--no-cpu]
+
+Workload (BASELINE.json north star): B=8, H=12, S=2048, D=64, bf16, non-causal, forward,
+unpadded layout (B*S, H, D), synthetic N(0,1) inputs resident in HBM. One step = one forward
+pass over the batch through the drop-in interface (flash_attn_unpadded_func -> C ABI ->
+fa_fwd_kernel). Multi-GPU: one process per GPU (torchrun), independent replicas (attention is
+per-sample, no collective); value = total FLOPs of all ranks / max time.
+
+Rank 0 prints ONE JSON line. `roofline` is the forward kernel: algorithmic FLOPs per launch
+(4*B*H*S*S*D) / its average duration from HIP events around each launch on the launch stream.
+`cpu_baseline` times the oracle's naive fp32 attention (restating benchmarks/
+benchmark_flash_attention.py:14-36 / tests/test_flash_attn.py:115-159) on the host cores on a
+bounded sample (2 of the 8 sequences). `extra` carries the other BASELINE.json configs.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hazyresearch_flash-attention_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 flop/clk x 2.4 GHz, dense (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def fwd_flops(B, H, Sq, Sk, D, causal):
+    f = 4.0 * B * H * Sq * Sk * D
+    return f / 2 if causal else f
+
+
+def fwd_bytes(B, H, Sq, Sk, D, elt=2):
+    return 2 * (B * Sq * H * D + B * Sk * H * D) * elt + 4 * B * H * Sq
+
+
+def make_inputs(B, H, Sq, Sk, D, dtype, dev, kvpacked=False, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    q = torch.randn(B * Sq, H, D, generator=g).to(dtype).to(dev)
+    if kvpacked:
+        kv = torch.randn(B * Sk, 2, H, D, generator=g).to(dtype).to(dev)
+        k, v = kv[:, 0], kv[:, 1]
+    else:
+        kv = None
+        k = torch.randn(B * Sk, H, D, generator=g).to(dtype).to(dev)
+        v = torch.randn(B * Sk, H, D, generator=g).to(dtype).to(dev)
+    cu_q = torch.arange(0, (B + 1) * Sq, Sq, dtype=torch.int32, device=dev)
+    cu_k = torch.arange(0, (B + 1) * Sk, Sk, dtype=torch.int32, device=dev)
+    return q, k, v, kv, cu_q, cu_k
+
+
+def time_events(fn, iters, warmup):
+    """Average device time of fn() from HIP events on torch's current stream (where the
+    library launches)."""
+    for _ in range(warmup):
+        fn()
+    s = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
+    for i in range(iters):
+        s[i].record()
+        fn()
+        e[i].record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in zip(s, e))
+    return sum(ts) / len(ts), ts[len(ts) // 2]
+
+
+def cpu_baseline(B, H, S, D):
+    """Oracle naive attention (fp32) on the host cores, bounded sample: 2 sequences."""
+    from oracle.attention_ref import attention_ref
+    nb = 2
+    g = torch.Generator().manual_seed(0)
+    q, k, v = (torch.randn(nb, S, H, D, generator=g).bfloat16() for _ in range(3))
+    attention_ref(q[:1, :256], k[:1, :256], v[:1, :256])  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        attention_ref(q, k, v)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el > 8.0 or reps >= 5:
+            break
+    flops = fwd_flops(nb, H, S, S, D, False) * reps
+    return {"value": round(flops / el / 1e12, 4), "unit": "TFLOPS", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle attention_ref fp32 (upcast) on {nb} of {B} sequences (B={nb},H={H},S={S},D={D}), "
+                      f"{reps} reps, {el:.2f}s"}
+
+
+def read_traffic():
+    """HBM bytes per forward launch from the committed PMC summary (profiles/*_fwd_pmc.json), or None."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    cands = sorted(f for f in os.listdir(pdir) if f.endswith("_fwd_pmc.json"))
+    if not cands:
+        return None
+    try:
+        with open(os.path.join(pdir, cands[-1])) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+
+    from flash_attn.flash_attn_interface import flash_attn_unpadded_func, flash_attn_unpadded_kvpacked_func
+
+    B, H, S, D = 8, 12, 2048, 64
+    dtype = torch.bfloat16
+    q, k, v, _, cu_q, cu_k = make_inputs(B, H, S, S, D, dtype, dev, seed=rank)
+    step = lambda: flash_attn_unpadded_func(q, k, v, cu_q, cu_k, S, S, 0.0)
+    flops = fwd_flops(B, H, S, S, D, False)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    value = world * flops * args.steps / el / 1e12
+
+    # kernel-level roofline: HIP events around each launch on the launch stream
+    avg_ms, med_ms = time_events(step, max(args.steps, 20), 3)
+    achieved = flops / (avg_ms * 1e-3) / 1e12
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": read_traffic(),
+                "kernel": "fa_fwd_kernel<64,bf16,noncausal,nodropout>", "avg_kernel_ms": round(avg_ms, 4),
+                "flops_per_launch": flops, "algorithmic_bytes_per_launch": fwd_bytes(B, H, S, S, D)}
+
+    extra = {}
+    if not args.no_extra and rank == 0:
+        def fwd_case(name, B_, H_, Sq_, Sk_, D_, dt, causal, p=0.0, kvpacked=False):
+            q_, k_, v_, kv_, cq, ck = make_inputs(B_, H_, Sq_, Sk_, D_, dt, dev, kvpacked=kvpacked)
+            if kvpacked:
+                fn = lambda: flash_attn_unpadded_kvpacked_func(q_, kv_, cq, ck, Sq_, Sk_, p, causal=causal)
+            else:
+                fn = lambda: flash_attn_unpadded_func(q_, k_, v_, cq, ck, Sq_, Sk_, p, causal=causal)
+            ms, _ = time_events(fn, 20, 5)
+            fl = fwd_flops(B_, H_, Sq_, Sk_, D_, causal)
+            extra[name] = {"ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2),
+                           "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
+            del q_, k_, v_, kv_
+
+        fwd_case("c2_B8_H12_S512_D64_fp16_fwd", 8, 12, 512, 512, 64, torch.float16, False)
+        fwd_case("c3_B8_H12_S2048_D64_bf16_causal_p0.1_fwd", 8, 12, 2048, 2048, 64, torch.bfloat16, True, 0.1)
+        fwd_case("c4_B16_H12_S4096_D128_bf16_causal_fwd", 16, 12, 4096, 4096, 128, torch.bfloat16, True)
+        fwd_case("c5_B4_H16_Sq1024_Sk4096_D64_bf16_kvpacked_fwd", 4, 16, 1024, 4096, 64, torch.bfloat16, False,
+                 kvpacked=True)
+        # C3 forward + backward (the fwd+bwd headline of the reference README charts)
+        q3, k3, v3, _, c3q, c3k = make_inputs(8, 12, 2048, 2048, 64, torch.bfloat16, dev)
+        q3.requires_grad_(); k3.requires_grad_(); v3.requires_grad_()
+        gout = torch.randn_like(q3)
+
+        def fb():
+            o = flash_attn_unpadded_func(q3, k3, v3, c3q, c3k, 2048, 2048, 0.1, causal=True)
+            torch.autograd.grad(o, (q3, k3, v3), gout)
+
+        ms, _ = time_events(fb, 10, 3)
+        fl = fwd_flops(8, 12, 2048, 2048, 64, True) * 3.5
+        extra["c3_B8_H12_S2048_D64_bf16_causal_p0.1_fwd_bwd"] = {
+            "ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2), "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
+
+    cpu = None
+    if not args.no_cpu and rank == 0 and world == 1:
+        cpu = cpu_baseline(B, H, S, D)
+
+    if rank == 0:
+        line = {
+            "metric": "attention fwd TFLOPS (and % of MI355X bf16 MFMA peak) at S=2048, D=64",
+            "value": round(value, 2), "unit": "TFLOPS", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic N(0,1) q/k/v resident in HBM",
+            "config": {"workload": "flash_attn_unpadded_func forward, B=8 H=12 S=2048 D=64 bf16 non-causal, p=0",
+                       "global_batch": B * world, "seq_len": S, "heads": H, "head_dim": D,
+                       "parallelism": f"replicas x{world} (no collective)"},
+            "frac_peak": round(value / world / PEAK_BF16_TFLOPS, 4),
+            "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -32,6 +32,7 @@ def hipcc():
 
 def common_flags():
     return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
+            "-mllvm", "-amdgpu-mfma-vgpr-form",  # keep MFMA C/D in VGPRs: no accvgpr shuffles
             "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
 

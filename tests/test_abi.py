@@ -1,0 +1,120 @@
+"""CPU tests of the drop-in boundary: libfa_hip.so loads, exports every symbol include/fa_hip.h
+declares, the ctypes struct layouts match the C ones, argument validation fails with error codes
+(no GPU call is made on those paths), and the Python surface mirrors the reference's names and
+signatures (flash_attn/flash_attn_interface.py:39-252)."""
+import ctypes
+import inspect
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "fa_hip.h")
+
+
+def _declared_functions():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(fa_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_entry_points():
+    assert _declared_functions() == ["fa_bwd", "fa_fwd", "fa_last_error", "fa_query", "fa_version"]
+
+
+def test_library_exports_every_declared_symbol():
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    for name in _declared_functions():
+        assert hasattr(L, name), name
+
+
+def test_struct_layouts_match():
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    assert L.fa_query(hip.FA_QUERY_FWD_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaFwdArgs)
+    assert L.fa_query(hip.FA_QUERY_BWD_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaBwdArgs)
+    assert L.fa_query(hip.FA_QUERY_MAX_HEAD_DIM, 0, 0, 0) == 128
+    assert L.fa_query(hip.FA_QUERY_BWD_WORKSPACE, 10, 2, 64) == 10 * 2 * 64 * 4
+    assert L.fa_query(999, 0, 0, 0) == -1
+    assert b"gfx950" in L.fa_version()
+
+
+def _valid_fwd_args(hip):
+    a = hip.FaFwdArgs()
+    a.q = a.k = a.v = a.o = a.softmax_lse = 4096
+    a.cu_seqlens_q = a.cu_seqlens_k = 4096
+    a.q_row_stride = a.k_row_stride = a.v_row_stride = a.o_row_stride = 128
+    a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = 64
+    a.batch, a.nheads, a.head_dim = 1, 2, 64
+    a.max_seqlen_q = a.max_seqlen_k = 0   # zero-size: returns before any launch
+    a.lse_stride = 16
+    a.softmax_scale = 0.125
+    a.dtype = hip.FA_DTYPE_BF16
+    return a
+
+
+@pytest.mark.parametrize("field,value,code", [
+    ("head_dim", 60, 2), ("head_dim", 136, 2), ("batch", 0, 1), ("nheads", 0, 1), ("dtype", 7, 1),
+    ("p_dropout", 1.0, 1), ("p_dropout", -0.1, 1), ("lse_stride", -1, 1), ("q", None, 1),
+    ("q_row_stride", 129, 1), ("softmax_scale", float("inf"), 1),
+])
+def test_fwd_argument_validation(field, value, code):
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    a = _valid_fwd_args(hip)
+    assert L.fa_fwd(ctypes.byref(a), None) == 0  # the valid zero-size call succeeds without a GPU
+    setattr(a, field, value)
+    rc = L.fa_fwd(ctypes.byref(a), None)
+    assert rc == code
+    assert len(L.fa_last_error()) > 0
+
+
+def test_null_args_pointer():
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    assert L.fa_fwd(None, None) == 1
+    assert L.fa_bwd(None, None) == 1
+    assert b"NULL" in L.fa_last_error()
+
+
+def test_last_error_is_thread_local():
+    import threading
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    L.fa_fwd(None, None)
+    seen = []
+    t = threading.Thread(target=lambda: seen.append(L.fa_last_error()))
+    t.start()
+    t.join()
+    assert seen == [b""]
+    assert L.fa_last_error() != b""
+
+
+def test_interface_mirrors_reference_signatures():
+    from flash_attn import flash_attn_interface as fi
+    sig = lambda f: list(inspect.signature(f).parameters)
+    assert sig(fi.flash_attn_unpadded_qkvpacked_func) == [
+        "qkv", "cu_seqlens", "max_seqlen", "dropout_p", "softmax_scale", "causal", "return_attn_probs"]
+    assert sig(fi.flash_attn_unpadded_kvpacked_func) == [
+        "q", "kv", "cu_seqlens_q", "cu_seqlens_k", "max_seqlen_q", "max_seqlen_k", "dropout_p", "softmax_scale",
+        "causal", "return_attn_probs"]
+    assert sig(fi.flash_attn_unpadded_func) == [
+        "q", "k", "v", "cu_seqlens_q", "cu_seqlens_k", "max_seqlen_q", "max_seqlen_k", "dropout_p", "softmax_scale",
+        "causal", "return_attn_probs"]
+    assert sig(fi.flash_attn_func) == ["qkv", "cu_seqlens", "dropout_p", "max_s", "softmax_scale", "causal",
+                                       "return_attn_probs"]
+    for cls in ("FlashAttnQKVPackedFunc", "FlashAttnKVPackedFunc", "FlashAttnFunc"):
+        assert hasattr(fi, cls)
+    from flash_attn import flash_attn_hip as hip
+    assert sig(hip.fwd)[:13] == ["q", "k", "v", "cu_seqlens_q", "cu_seqlens_k", "max_seqlen_q", "max_seqlen_k",
+                                 "p_dropout", "softmax_scale", "zero_tensors", "is_causal", "return_softmax", "gen"]
+
+
+def test_python_checks_raise_runtime_error_on_cpu_tensors():
+    import torch
+    from flash_attn import flash_attn_interface as fi
+    q = torch.randn(16, 2, 64, dtype=torch.float16)
+    cu = torch.tensor([0, 16], dtype=torch.int32)
+    with pytest.raises(RuntimeError):
+        fi.flash_attn_unpadded_func(q, q, q, cu, cu, 16, 16, 0.0)

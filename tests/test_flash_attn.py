@@ -120,7 +120,7 @@ DIMS = [32, 56, 64, 80, 96, 128]
 @pytest.mark.parametrize("seqlen", [97, 128, 257, 512])
 @pytest.mark.parametrize("dropout_p", [0.0, 0.17])
 def test_flash_attn_unpadded(seqlen, d, dropout_p, causal, dtype):
-    run_case("separate", 8, seqlen, seqlen, 4, d, dtype, causal, dropout_p)
+    run_case("separate", 32, seqlen, seqlen, 4, d, dtype, causal, dropout_p)
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
@@ -129,7 +129,7 @@ def test_flash_attn_unpadded(seqlen, d, dropout_p, causal, dtype):
 @pytest.mark.parametrize("seqlen", [200, 384, 1025])
 @pytest.mark.parametrize("dropout_p", [0.0, 0.17])
 def test_flash_attn_unpadded_qkvpacked(seqlen, d, dropout_p, causal, dtype):
-    run_case("qkvpacked", 8, seqlen, seqlen, 4, d, dtype, causal, dropout_p)
+    run_case("qkvpacked", 32, seqlen, seqlen, 4, d, dtype, causal, dropout_p)
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
