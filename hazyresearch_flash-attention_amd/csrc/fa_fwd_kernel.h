@@ -10,13 +10,18 @@
 //   - var-len sequences through cu_seqlens             csrc/flash_attn/src/fmha_kernel.h:45-76
 //
 // MI355X-first structure (NOT the reference's FA-1 loop order): FA-2 order, grid =
-// (q-blocks, H, B); a workgroup = 4 waves = 128 query rows, one wave = 32 rows. Q stays in
-// VGPRs for the whole kernel; K/V tiles of 64 keys are register-staged into a double-buffered,
-// XOR-swizzled LDS image (issue-early / write-late, one barrier per tile). Scores are computed
-// swapped (S^T = K Q^T, v_mfma_f32_32x32x16) so each lane owns one query row: the row max is
-// 31 fmax + one v_permlane32_swap, the row sum stays lane-local until the epilogue, and P feeds
-// the P·V MFMA straight from registers (accumulator-as-B-operand). V^T operands come from
-// ds_read_b64_tr_b16. The N x N score matrix never leaves registers.
+// (q-blocks, H, B) remapped so that all q-blocks of one head run on one XCD (its K/V stay in
+// that XCD's L2). A workgroup = 8 waves = 256 query rows, one wave = 32 rows. Q stays in VGPRs;
+// K/V tiles of 64 keys are loaded with bounds-checked buffer loads (out-of-range -> 0, no
+// branches) into registers early and written late into a double-buffered, XOR-swizzled LDS
+// image (one barrier per tile). The loop is unrolled by two so every LDS address is a
+// lane-constant base plus an immediate. Scores are computed swapped (S^T = K Q^T,
+// v_mfma_f32_32x32x16) so each lane owns one query row: the row max is a tree of v_max3 plus one
+// v_permlane32_swap, the row sum stays lane-local until the epilogue, and P feeds the P·V MFMA
+// straight from registers (accumulator-as-B-operand); V^T operands come from
+// ds_read_b64_tr_b16. The running max is only moved when it grows by more than 2^8 (T13,
+// deferred rescale): O and l are rescaled rarely, P stays <= 256. The N x N score matrix never
+// leaves registers.
 #pragma once
 
 #include "fa_common.h"
@@ -24,31 +29,111 @@
 
 namespace fa {
 
+// Structure switches (compile-time; tools/fwd_variants.py builds and A/B-times combinations).
+#ifndef FA_FWD_PIPE
+#define FA_FWD_PIPE 0      // 1: software-pipeline QK^T of tile j+1 under the softmax of tile j (T15)
+#endif
+#ifndef FA_FWD_SCHED
+#define FA_FWD_SCHED 0     // 1: pin the MFMA/VALU interleave with sched_group_barrier (T19)
+#endif
+#ifndef FA_FWD_NW
+#define FA_FWD_NW 8        // waves per workgroup (32 query rows each)
+#endif
+#ifndef FA_FWD_WPS
+#define FA_FWD_WPS 0       // >0: __launch_bounds__ minimum waves per SIMD
+#endif
+
 template <int D>
 struct FwdCfg {
-    static constexpr int NW = 4;                  // waves per workgroup
+    static constexpr int NW = FA_FWD_NW;          // waves per workgroup
+    static constexpr int NT = 64 * NW;            // threads per workgroup
     static constexpr int BM = 32 * NW;            // query rows per workgroup
     static constexpr int BN = 64;                 // keys per iteration
     static constexpr int NC = D / 8;              // 16-B chunks per row
     static constexpr int TILE_BYTES = BN * D * 2;
-    static constexpr int CPT = BN * NC / 256;     // staged chunks per thread per tile
+    static constexpr int CPT = (BN * NC + NT - 1) / NT;   // staged chunks per thread per tile
     static constexpr int RNG_BYTES_PER_WAVE = 2 * 32 * 32 * 2;  // two 32x32 u16 images
     static constexpr int lds_bytes(bool dropout) {
         return 4 * TILE_BYTES + (dropout ? NW * RNG_BYTES_PER_WAVE : 0);
     }
 };
 
+// log2-domain threshold of the deferred rescale: P values stay below 2^RESCALE_THR.
+constexpr float RESCALE_THR = 8.0f;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload128(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+constexpr int OOB = (int)0x80000000;  // any offset past num_records reads as zero
+
+// v_max3_f32 as one instruction (plain fmaxf at -O3 adds NaN-canonicalising v_max x,x first).
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// max of 32 values: 4 independent chains of v_max3 (ILP 4), 18 instructions.
+__device__ __forceinline__ float max_tree32(const f32x16 &a, const f32x16 &b) {
+    float acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float x0 = a[4 * k], x1 = a[4 * k + 1], x2 = a[4 * k + 2], x3 = a[4 * k + 3];
+        const float y0 = b[4 * k], y1 = b[4 * k + 1], y2 = b[4 * k + 2], y3 = b[4 * k + 3];
+        float m = max3f(x0, x1, x2);
+        m = max3f(m, x3, y0);
+        m = max3f(m, y1, y2);
+        acc[k] = max3f(m, y3, y3);
+    }
+    return max3f(max3f(acc[0], acc[1], acc[2]), acc[3], acc[3]);
+}
+__device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
+    float t[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[i] = a[i] + b[i];
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; ++i) t[i] = t[i] + t[i + w];
+    return t[0];
+}
+
+#if FA_FWD_WPS > 0
+#define FA_FWD_BOUNDS __launch_bounds__(64 * FA_FWD_NW, FA_FWD_WPS)
+#else
+#define FA_FWD_BOUNDS __launch_bounds__(64 * FA_FWD_NW)
+#endif
+
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
-__global__ __launch_bounds__(256) void fa_fwd_kernel(const FaFwdArgs a) {
+__global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
     using C = FwdCfg<D>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
-    const int b = blockIdx.z;
-    const int h = blockIdx.y;
-    // causal: heaviest query blocks first (LPT order)
-    const int qb = CAUSAL ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+    // ---- block -> (q-block, head, batch)
+    const int nqb = gridDim.x;
+    const int nbh = gridDim.y * gridDim.z;
+    const int nwg = nqb * nbh;
+    const int L = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
+    int qb, bh_lin;
+    if (CAUSAL) {
+        // global LPT order: the heaviest (last) query blocks of every head first
+        qb = nqb - 1 - L / nbh;
+        bh_lin = L % nbh;
+    } else {
+        // XCD-aware: blocks L and L+8 share an XCD; give each XCD a contiguous run of
+        // (head, q-block) so a head's K/V are fetched into one L2 (bijective for any nwg).
+        const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
+        const int Lp = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+        qb = Lp % nqb;
+        bh_lin = Lp / nqb;
+    }
+    const int h = bh_lin % a.nheads;
+    const int b = bh_lin / a.nheads;
+
     const int q_start = a.cu_seqlens_q[b];
     const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
     const int k_start = a.cu_seqlens_k[b];
@@ -65,14 +150,9 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const FaFwdArgs a) {
     const int qrow = qw + l32;           // the query row this lane owns
     const int head_dim = a.head_dim;
 
-    const uint16_t *qp = (const uint16_t *)a.q + (int64_t)q_start * a.q_row_stride + (int64_t)h * a.q_head_stride;
-    const uint16_t *kp = (const uint16_t *)a.k + (int64_t)k_start * a.k_row_stride + (int64_t)h * a.k_head_stride;
-    const uint16_t *vp = (const uint16_t *)a.v + (int64_t)k_start * a.v_row_stride + (int64_t)h * a.v_head_stride;
-
-    char *kbuf0 = smem;
-    char *kbuf1 = smem + C::TILE_BYTES;
-    char *vbuf0 = smem + 2 * C::TILE_BYTES;
-    char *vbuf1 = smem + 3 * C::TILE_BYTES;
+    const auto qr = make_rsrc((const uint16_t *)a.q + (int64_t)q_start * a.q_row_stride + (int64_t)h * a.q_head_stride);
+    const auto kr = make_rsrc((const uint16_t *)a.k + (int64_t)k_start * a.k_row_stride + (int64_t)h * a.k_head_stride);
+    const auto vr = make_rsrc((const uint16_t *)a.v + (int64_t)k_start * a.v_row_stride + (int64_t)h * a.v_head_stride);
 
     int n_end = seqlen_k;
     if (CAUSAL) n_end = min(n_end, q0 + C::BM);
@@ -83,33 +163,49 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const FaFwdArgs a) {
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
         const int c = 2 * ks + hi;
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (qrow < seqlen_q && c * 8 < head_dim) v = gload128(qp + (int64_t)qrow * a.q_row_stride + c * 8);
-        qf[ks] = as_frag<T>(v);
+        const bool ok = qrow < seqlen_q && c * 8 < head_dim;
+        qf[ks] = as_frag<T>(bload128(qr, ok ? (qrow * (int)a.q_row_stride + c * 8) * 2 : OOB));
     }
 
-    // ---- register staging of one K/V tile (issue early, write late: T14)
+    // ---- register staging of K/V tiles (issue early, write late: T14). Loads are bounds-checked
+    // buffer loads: a tile past the end reads as zeros, so no branch is needed around them.
+    int st_off_k[C::CPT], st_off_v[C::CPT], st_lds[C::CPT], st_row[C::CPT], st_okc[C::CPT];
+#pragma unroll
+    for (int i = 0; i < C::CPT; ++i) {
+        const int idx = tid + C::NT * i;
+        const int row = idx / C::NC, c = idx % C::NC;
+        st_row[i] = idx < C::BN * C::NC ? row : (1 << 20);   // surplus threads load nothing
+        st_okc[i] = c * 8 < head_dim;
+        st_off_k[i] = (row * (int)a.k_row_stride + c * 8) * 2;
+        st_off_v[i] = (row * (int)a.v_row_stride + c * 8) * 2;
+        st_lds[i] = S::off(row, c);
+    }
+    const int k_tile_step = C::BN * (int)a.k_row_stride * 2;
+    const int v_tile_step = C::BN * (int)a.v_row_stride * 2;
     u32x4 kst[C::CPT], vst[C::CPT];
-    auto gload_tile = [&](int kv0) {
+    auto gload_k = [&](int j) {
 #pragma unroll
         for (int i = 0; i < C::CPT; ++i) {
-            const int idx = tid + 256 * i;
-            const int row = idx / C::NC, c = idx % C::NC;
-            const int kv = kv0 + row;
-            const bool ok = kv < seqlen_k && c * 8 < head_dim;
-            u32x4 z = {0u, 0u, 0u, 0u};
-            kst[i] = ok ? gload128(kp + (int64_t)kv * a.k_row_stride + c * 8) : z;
-            vst[i] = ok ? gload128(vp + (int64_t)kv * a.v_row_stride + c * 8) : z;
+            const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
+            kst[i] = bload128(kr, ok ? st_off_k[i] + j * k_tile_step : OOB);
         }
     };
-    auto lds_store_tile = [&](char *kb, char *vb) {
+    auto gload_v = [&](int j) {
 #pragma unroll
         for (int i = 0; i < C::CPT; ++i) {
-            const int idx = tid + 256 * i;
-            const int row = idx / C::NC, c = idx % C::NC;
-            lds_write128(kb, S::off(row, c), kst[i]);
-            lds_write128(vb, S::off(row, c), vst[i]);
+            const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
+            vst[i] = bload128(vr, ok ? st_off_v[i] + j * v_tile_step : OOB);
         }
+    };
+    auto lds_store_k = [&](char *kb) {
+#pragma unroll
+        for (int i = 0; i < C::CPT; ++i)
+            if ((C::BN * C::NC) % C::NT == 0 || tid + C::NT * i < C::BN * C::NC) lds_write128(kb, st_lds[i], kst[i]);
+    };
+    auto lds_store_v = [&](char *vb) {
+#pragma unroll
+        for (int i = 0; i < C::CPT; ++i)
+            if ((C::BN * C::NC) % C::NT == 0 || tid + C::NT * i < C::BN * C::NC) lds_write128(vb, st_lds[i], vst[i]);
     };
 
     f32x16 o[D / 32];
@@ -133,34 +229,61 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const FaFwdArgs a) {
     const int qq = (lane & 15) >> 2;
     const int pp = lane & 3;
 
-    if (nt > 0) {
-        gload_tile(0);
-        lds_store_tile(kbuf0, vbuf0);
-    }
-    __syncthreads();
-
-    for (int j = 0; j < nt; ++j) {
-        const int kv0 = j * C::BN;
-        const bool odd = j & 1;
-        char *kb = odd ? kbuf1 : kbuf0;
-        char *vb = odd ? vbuf1 : vbuf0;
-        if (j + 1 < nt) gload_tile(kv0 + C::BN);
-
-        const bool active = (qw < seqlen_q) && (!CAUSAL || kv0 <= qw + 31);
-        if (active) {
-            // ---- S^T = K Q^T : two 32x32 sub-tiles, lane = query row, registers = keys
-            f32x16 s[2];
+    // lane-constant LDS offsets (the per-buffer base and k-step/tile parts fold into immediates)
+    int k_rd[2][D / 16];
 #pragma unroll
-            for (int st = 0; st < 2; ++st) {
+    for (int st = 0; st < 2; ++st)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) s[st][r] = 0.f;
+        for (int ks = 0; ks < D / 16; ++ks) k_rd[st][ks] = S::off(32 * st + l32, 2 * ks + hi);
+    int v_rd[D / 32][2][2][2];
 #pragma unroll
-                for (int ks = 0; ks < D / 16; ++ks) {
-                    u32x4 kf = lds_read128(kb, S::off(32 * st + l32, 2 * ks + hi));
-                    s[st] = T::mfma32(as_frag<T>(kf), qf[ks], s[st]);
-                }
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int rb = 32 * st + 16 * s2 + 4 * hi + qq;
+                const int col = 32 * dt + 16 * grp + 4 * pp;
+                v_rd[dt][st][s2][0] = S::off8(rb, col);
+                v_rd[dt][st][s2][1] = S::off8(rb + 8, col);
             }
-            // ---- mask (only on the ragged last tile and the causal diagonal)
+
+    // S^T = K Q^T for one 64-key tile: two 32x32 sub-tiles, lane = query row, registers = keys
+    auto qk = [&](const char *kb, f32x16 (&s)[2]) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[st][r] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < D / 16; ++ks)
+                s[st] = T::mfma32(as_frag<T>(lds_read128(kb, k_rd[st][ks])), qf[ks], s[st]);
+        }
+    };
+
+    // Software pipeline (T15): while the VALU runs the softmax of tile j, the matrix pipe
+    // computes S of tile j+1. K runs one tile ahead of V in LDS:
+    //   iteration j (parity P): reads K[j+1] from kbuf[1-P], V[j] from vbuf[P];
+    //   stages K[j+2] -> kbuf[P] and V[j+1] -> vbuf[1-P]; one barrier.
+    f32x16 sA[2], sB[2];   // S of even / odd tiles
+    auto step = [&](auto par_tag, int j) {
+        constexpr int P = decltype(par_tag)::value;
+        f32x16 (&s)[2] = P == 0 ? sA : sB;       // this tile's scores
+        f32x16 (&sn)[2] = P == 0 ? sB : sA;      // next tile's scores
+        constexpr bool PIPE = FA_FWD_PIPE;
+        // pipelined: K one tile ahead (read K[j+1] from kbuf[1-P], stage K[j+2] into kbuf[P]);
+        // plain: K[j], V[j] in buffer P, stage tile j+1 into buffer 1-P.
+        char *kb_rd = smem + (PIPE ? 1 - P : P) * C::TILE_BYTES;
+        char *vb_rd = smem + (2 + P) * C::TILE_BYTES;
+        char *kb_wr = smem + (PIPE ? P : 1 - P) * C::TILE_BYTES;
+        char *vb_wr = smem + (3 - P) * C::TILE_BYTES;
+        const int kv0 = j * C::BN;
+        gload_k(PIPE ? j + 2 : j + 1);
+        gload_v(j + 1);
+        if constexpr (!PIPE) qk(kb_rd, s);
+
+        {
+            // ---- mask (only on the ragged last tile and the causal diagonal; a tile entirely
+            // above the diagonal for this wave comes out all -inf, i.e. contributes zeros)
             const bool need_mask = (kv0 + C::BN > seqlen_k) || (CAUSAL && kv0 + C::BN - 1 > qw);
             if (need_mask) {
 #pragma unroll
@@ -171,36 +294,35 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const FaFwdArgs a) {
                         if (kv >= seqlen_k || (CAUSAL && kv > qrow)) s[st][r] = -INFINITY;
                     }
             }
-            // ---- online softmax
-            float mx = s[0][0];
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[st][r]);
-            mx = pair_max(mx);
+            // ---- online softmax with deferred rescale
+            const float mx = pair_max(max_tree32(s[0], s[1]));
             const float m_new = fmaxf(m_i, mx);
-            const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-            const float mc = m_use * c_log2;
-            const float alpha = fast_exp2(m_i * c_log2 - mc);
-            float rs = 0.f;
+            const bool grow = (m_new - m_i) * c_log2 > RESCALE_THR;   // NaN (all -inf) -> false
+            if (__builtin_amdgcn_ballot_w64(grow)) {
+                const float alpha = grow ? fast_exp2((m_i - m_new) * c_log2) : 1.f;
+                if (grow) m_i = m_new;
+                l_i *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            }
+        }
+        // ---- branch-free from here to the barrier (one scheduling region): the next tile's
+        // scores on the matrix pipe interleaved with this tile's exp/sum/convert on the VALU.
+        // Inactive (fully masked) tiles compute zeros: their scores are -inf.
+        if constexpr (PIPE) qk(kb_rd, sn);
+        {
+            const float mc = (m_i == -INFINITY ? 0.f : m_i) * c_log2;
 #pragma unroll
             for (int st = 0; st < 2; ++st)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float p = fast_exp2(fmaf(s[st][r], c_log2, -mc));
-                    s[st][r] = p;
-                    rs += p;
-                }
-            l_i = l_i * alpha + rs;
-            m_i = m_new;
-#pragma unroll
-            for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+                for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
+            l_i += sum_tree32(s[0], s[1]);
 
             if (DROPOUT) {
-                // Generate the keep mask in the column-major (backward) layout, then transpose
-                // it through a per-wave LDS image with ds_read_b64_tr_b16.
+                // Keep mask generated in the column-major (backward) layout, transposed through a
+                // per-wave LDS image with ds_read_b64_tr_b16.
 #pragma unroll
                 for (int st = 0; st < 2; ++st) {
                     char *img = rng_img + st * (32 * 32 * 2);
@@ -243,23 +365,53 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const FaFwdArgs a) {
                 }
             // ---- O^T += V^T P^T
 #pragma unroll
-            for (int dt = 0; dt < D / 32; ++dt) {
-                const int col = 32 * dt + 16 * grp + 4 * pp;
+            for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
                 for (int st = 0; st < 2; ++st)
 #pragma unroll
                     for (int s2 = 0; s2 < 2; ++s2) {
-                        const int rb = 32 * st + 16 * s2 + 4 * hi + qq;
-                        u32x2 lo = lds_read_tr(vb, S::off8(rb, col));
-                        u32x2 hv = lds_read_tr(vb, S::off8(rb + 8, col));
+                        u32x2 lo = lds_read_tr(vb_rd, v_rd[dt][st][s2][0]);
+                        u32x2 hv = lds_read_tr(vb_rd, v_rd[dt][st][s2][1]);
                         u32x4 av = {lo[0], lo[1], hv[0], hv[1]};
                         o[dt] = T::mfma32(as_frag<T>(av), pf[st][s2], o[dt]);
                     }
+        }
+        if constexpr (!DROPOUT && FA_FWD_SCHED && PIPE) {
+            // pin the interleave (T19): all next-tile K reads first; then per next-tile MFMA two
+            // V^T transposed reads and ~10 softmax VALU ops; then the P·V MFMAs with the rest.
+            constexpr int NQK = 2 * (D / 16), NPV = 4 * (D / 32);
+            __builtin_amdgcn_sched_group_barrier(0x100, NQK, 0);
+#pragma unroll
+            for (int i = 0; i < NQK; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, (2 * NPV) / NQK, 0);
+                __builtin_amdgcn_sched_group_barrier(0x402, 88 / NQK, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < NPV; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x402, 4, 0);
             }
         }
-
-        if (j + 1 < nt) lds_store_tile(odd ? kbuf0 : kbuf1, odd ? vbuf0 : vbuf1);
+        lds_store_k(kb_wr);
+        lds_store_v(vb_wr);
         __syncthreads();
+    };
+
+    // prologue: K[0] -> kbuf0, V[0] -> vbuf0 (+ K[1] -> kbuf1 and S of tile 0 when pipelined)
+    gload_k(0);
+    gload_v(0);
+    lds_store_k(smem);
+    lds_store_v(smem + 2 * C::TILE_BYTES);
+    if (FA_FWD_PIPE) {
+        gload_k(1);
+        lds_store_k(smem + C::TILE_BYTES);
+    }
+    __syncthreads();
+    if (FA_FWD_PIPE) qk(smem, sA);
+    for (int j = 0; j < nt; j += 2) {
+        step(std::integral_constant<int, 0>(), j);
+        if (j + 1 < nt) step(std::integral_constant<int, 1>(), j + 1);
     }
 
     // ---- epilogue

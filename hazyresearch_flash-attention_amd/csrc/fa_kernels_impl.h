@@ -15,7 +15,7 @@ static hipError_t launch_fwd_t(const FaFwdArgs &a, hipStream_t stream) {
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (attr_err != hipSuccess) return attr_err;
     dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
+    hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a);
     return hipGetLastError();
 }
 

@@ -1,0 +1,152 @@
+"""A/B harness for forward-kernel structure variants (guide rule 24: interleaved rounds, one process).
+
+    python tools/fwd_variants.py build            # here: compile build/var_<name>.so per variant
+    python tools/fwd_variants.py run [--rounds 5]  # on the GPU box: time every variant, interleaved
+
+Each variant recompiles only the head-dim TUs with its -D switches (FA_FWD_PIPE, FA_FWD_SCHED,
+FA_FWD_NW, FA_FWD_WPS) and links them with the shared objects of the main build. The run
+loads each library with ctypes (RTLD_LOCAL) and calls fa_fwd on the same device tensors.
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import concurrent.futures as cf
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "hazyresearch_flash-attention_amd")
+sys.path.insert(0, PKG)
+BUILD = os.path.join(PKG, "build")
+
+VARIANTS = {
+    "base": {},
+    "pipe": {"FA_FWD_PIPE": 1},
+    "pipe_sched": {"FA_FWD_PIPE": 1, "FA_FWD_SCHED": 1},
+    "nw8": {"FA_FWD_NW": 8},
+    "nw8_pipe": {"FA_FWD_NW": 8, "FA_FWD_PIPE": 1},
+    "wps3": {"FA_FWD_WPS": 3},
+    "nw8_wps2": {"FA_FWD_NW": 8, "FA_FWD_WPS": 2},
+}
+
+CONFIGS = [
+    # name, B, H, Sq, Sk, D, causal, dtype
+    ("ns_B8_H12_S2048_D64", 8, 12, 2048, 2048, 64, False, "bf16"),
+    ("c4_B16_H12_S4096_D128_causal", 16, 12, 4096, 4096, 128, True, "bf16"),
+    ("c5_B4_H16_1024x4096_D64", 4, 16, 1024, 4096, 64, False, "bf16"),
+]
+
+
+def build(names):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("fa_build", os.path.join(PKG, "build.py"))
+    fb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fb)
+    fb.build(verbose=False)
+    shared = [os.path.join(BUILD, s + ".o") for s in ("fa_api.cpp", "fa_aux.hip")]
+
+    def one(name):
+        defs = VARIANTS[name]
+        extra = [f"-D{k}={v}" for k, v in defs.items()]
+        objs = []
+        for tu in ("fa_d32.hip", "fa_d64.hip", "fa_d128.hip"):
+            obj = os.path.join(BUILD, f"var_{name}_{tu}.o")
+            cmd = [fb.hipcc()] + fb.common_flags() + extra + ["-x", "hip", "-c", os.path.join(fb.CSRC, tu), "-o", obj]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode:
+                raise RuntimeError(r.stderr)
+            objs.append(obj)
+        out = os.path.join(BUILD, f"var_{name}.so")
+        r = subprocess.run([fb.hipcc(), f"--offload-arch={fb.ARCH}", "-shared", "-fPIC", "-o", out] + shared + objs,
+                           capture_output=True, text=True)
+        if r.returncode:
+            raise RuntimeError(r.stderr)
+        return out
+
+    with cf.ThreadPoolExecutor(4) as ex:
+        for out in ex.map(one, names):
+            print("built", out)
+
+
+def run(names, rounds, iters):
+    import torch
+    from flash_attn import flash_attn_hip as hip
+    libs = {}
+    for n in names:
+        L = ctypes.CDLL(os.path.join(BUILD, f"var_{n}.so"))
+        L.fa_fwd.argtypes = [ctypes.POINTER(hip.FaFwdArgs), ctypes.c_void_p]
+        L.fa_fwd.restype = ctypes.c_int
+        libs[n] = L
+    results = {}
+    for (cname, B, H, Sq, Sk, D, causal, dt) in CONFIGS:
+        dtype = torch.bfloat16 if dt == "bf16" else torch.float16
+        g = torch.Generator().manual_seed(0)
+        q = torch.randn(B * Sq, H, D, generator=g).to(dtype).cuda()
+        k = torch.randn(B * Sk, H, D, generator=g).to(dtype).cuda()
+        v = torch.randn(B * Sk, H, D, generator=g).to(dtype).cuda()
+        cq = torch.arange(0, (B + 1) * Sq, Sq, dtype=torch.int32, device="cuda")
+        ck = torch.arange(0, (B + 1) * Sk, Sk, dtype=torch.int32, device="cuda")
+        ref, _lse = hip.fwd(q, k, v, cq, ck, Sq, Sk, 0.0, D ** -0.5, False, causal, False, None)
+        outs = {}
+        a = hip.FaFwdArgs()
+        lse = torch.empty(B, H, (Sq + 15) // 16 * 16, dtype=torch.float32, device="cuda")
+        a.q, a.k, a.v = q.data_ptr(), k.data_ptr(), v.data_ptr()
+        a.softmax_lse = lse.data_ptr()
+        a.cu_seqlens_q, a.cu_seqlens_k = cq.data_ptr(), ck.data_ptr()
+        a.q_row_stride, a.q_head_stride = q.stride(0), q.stride(1)
+        a.k_row_stride, a.k_head_stride = k.stride(0), k.stride(1)
+        a.v_row_stride, a.v_head_stride = v.stride(0), v.stride(1)
+        a.o_row_stride, a.o_head_stride = q.stride(0), q.stride(1)
+        a.batch, a.nheads, a.head_dim = B, H, D
+        a.max_seqlen_q, a.max_seqlen_k, a.lse_stride = Sq, Sk, lse.shape[2]
+        a.softmax_scale = D ** -0.5
+        a.is_causal = 1 if causal else 0
+        a.dtype = hip.FA_DTYPE_BF16 if dt == "bf16" else hip.FA_DTYPE_FP16
+        stream = torch.cuda.current_stream().cuda_stream
+        for n in names:
+            o = torch.empty_like(q)
+            outs[n] = o
+        times = {n: [] for n in names}
+        flops = 4.0 * B * H * Sq * Sk * D / (2 if causal else 1)
+        for r in range(rounds):
+            for n in names:
+                a.o = outs[n].data_ptr()
+                L = libs[n]
+                for _ in range(3):
+                    L.fa_fwd(ctypes.byref(a), stream)
+                s = torch.cuda.Event(enable_timing=True)
+                e = torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(iters):
+                    rc = L.fa_fwd(ctypes.byref(a), stream)
+                e.record()
+                torch.cuda.synchronize()
+                assert rc == 0
+                times[n].append(s.elapsed_time(e) / iters)
+        res = {}
+        for n in names:
+            ts = sorted(times[n])
+            err = (outs[n].float() - ref.float()).abs().max().item()
+            res[n] = {"ms_med": round(ts[len(ts) // 2], 4), "ms_min": round(ts[0], 4),
+                      "TFLOPS_med": round(flops / ts[len(ts) // 2] / 1e9, 1), "max_diff_vs_main": err}
+        results[cname] = res
+        print(cname, json.dumps(res), flush=True)
+    return results
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["build", "run"])
+    ap.add_argument("--only", default="")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    names = [n for n in VARIANTS if not args.only or n in args.only.split(",")]
+    if args.mode == "build":
+        build(names)
+    else:
+        out = run(names, args.rounds, args.iters)
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", "variants.json"), "w") as f:
+            json.dump(out, f, indent=1)
