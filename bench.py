@@ -55,20 +55,24 @@ def make_inputs(B, H, Sq, Sk, D, dtype, dev, kvpacked=False, seed=0):
     return q, k, v, kv, cu_q, cu_k
 
 
-def time_events(fn, iters, warmup):
-    """Average device time of fn() from HIP events on torch's current stream (where the
-    library launches)."""
+def time_events(fn, iters, warmup, reps=5):
+    """Average device time per call of fn(): HIP events on torch's current stream (where the
+    library launches) around `iters` back-to-back calls, median of `reps` batches."""
     for _ in range(warmup):
         fn()
-    s = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
-    for i in range(iters):
-        s[i].record()
-        fn()
-        e[i].record()
     torch.cuda.synchronize()
-    ts = sorted(a.elapsed_time(b) for a, b in zip(s, e))
-    return sum(ts) / len(ts), ts[len(ts) // 2]
+    per = []
+    for _ in range(reps):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        per.append(s.elapsed_time(e) / iters)
+    per.sort()
+    return per[len(per) // 2], per[0]
 
 
 def cpu_baseline(B, H, S, D):
@@ -155,7 +159,7 @@ def main():
     value = world * flops * args.steps / el / 1e12
 
     # kernel-level roofline: HIP events around each launch on the launch stream
-    avg_ms, med_ms = time_events(step, max(args.steps, 20), 3)
+    avg_ms, min_ms = time_events(step, max(args.steps, 20), 3)
     achieved = flops / (avg_ms * 1e-3) / 1e12
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": read_traffic(),
@@ -170,7 +174,7 @@ def main():
                 fn = lambda: flash_attn_unpadded_kvpacked_func(q_, kv_, cq, ck, Sq_, Sk_, p, causal=causal)
             else:
                 fn = lambda: flash_attn_unpadded_func(q_, k_, v_, cq, ck, Sq_, Sk_, p, causal=causal)
-            ms, _ = time_events(fn, 20, 5)
+            ms, _ = time_events(fn, 10, 3)
             fl = fwd_flops(B_, H_, Sq_, Sk_, D_, causal)
             extra[name] = {"ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2),
                            "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
@@ -190,7 +194,7 @@ def main():
             o = flash_attn_unpadded_func(q3, k3, v3, c3q, c3k, 2048, 2048, 0.1, causal=True)
             torch.autograd.grad(o, (q3, k3, v3), gout)
 
-        ms, _ = time_events(fb, 10, 3)
+        ms, _ = time_events(fb, 5, 2)
         fl = fwd_flops(8, 12, 2048, 2048, 64, True) * 3.5
         extra["c3_B8_H12_S2048_D64_bf16_causal_p0.1_fwd_bwd"] = {
             "ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2), "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}

@@ -9,9 +9,11 @@ the autograd layer can replay a forward's dropout mask without saving the whole 
 The library is loaded with ctypes (plain C ABI, include/fa_hip.h). There is no CPU fallback:
 if the shared object is missing every call raises.
 """
+import contextlib
 import ctypes
 import math
 import os
+import threading
 
 import torch
 
@@ -125,6 +127,25 @@ def _stream_ptr(device):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_tls = threading.local()
+
+
+def _args(kind):
+    # one reusable ctypes struct per host thread: the C side copies it at launch
+    a = getattr(_tls, kind, None)
+    if a is None:
+        a = FaFwdArgs() if kind == "fwd" else FaBwdArgs()
+        setattr(_tls, kind, a)
+    return a
+
+
+def _on_device(dev):
+    # the reference runs under a CUDAGuard for q's device (fmha_api.cpp:184)
+    if dev.index is None or dev.index == torch.cuda.current_device():
+        return contextlib.nullcontext()
+    return torch.cuda.device(dev)
+
+
 def reserve_rng(device, gen=None, increment=None):
     """Reserve a Philox (seed, offset) pair from the torch generator, like
     `gen->philox_cuda_state(counter_offset)` under the generator mutex (fmha_api.cpp:228-235)."""
@@ -168,7 +189,7 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
     max_seqlen_k = int(max_seqlen_k)
     dev = q.device
 
-    with torch.cuda.device(dev):
+    with _on_device(dev):
         o = torch.empty((total_q, nheads, head_dim), dtype=q.dtype, device=dev)
         lse_stride = max(_round16(max_seqlen_q), 16)
         lse = torch.empty((batch, nheads, lse_stride), dtype=torch.float32, device=dev)
@@ -184,7 +205,7 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
             seed, offset = rng_state if rng_state is not None else reserve_rng(dev, gen)
         else:
             seed, offset = 0, 0
-        a = FaFwdArgs()
+        a = _args("fwd")
         a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
         a.softmax_lse = lse.data_ptr()
         a.s_dmask = s.data_ptr() if s is not None else None
@@ -195,8 +216,7 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
         a.o_row_stride, a.o_head_stride = o.stride(0), o.stride(1)
         a.batch, a.nheads, a.head_dim = batch, nheads, head_dim
         a.max_seqlen_q, a.max_seqlen_k, a.lse_stride = max_seqlen_q, max_seqlen_k, lse_stride
-        if s is not None:
-            a.s_rows, a.s_cols = s.shape[2], s.shape[3]
+        a.s_rows, a.s_cols = (s.shape[2], s.shape[3]) if s is not None else (0, 0)
         a.softmax_scale = float(softmax_scale)
         a.p_dropout = float(p_dropout)
         a.rng_seed, a.rng_offset = seed, offset
@@ -232,7 +252,7 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
     _check(tuple(dk.shape) == tuple(k.shape) and tuple(dv.shape) == tuple(v.shape), "dk/dv must match k/v")
     lse_stride = softmax_lse.shape[-1]
     dev = q.device
-    with torch.cuda.device(dev):
+    with _on_device(dev):
         if zero_tensors:
             dq.zero_()
             dk.zero_()
@@ -246,7 +266,7 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
             seed, offset = rng_state if rng_state is not None else reserve_rng(dev, gen)
         else:
             seed, offset = 0, 0
-        a = FaBwdArgs()
+        a = _args("bwd")
         a.dout, a.q, a.k, a.v, a.out = dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
         a.softmax_lse = softmax_lse.data_ptr()
         a.dq, a.dk, a.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
