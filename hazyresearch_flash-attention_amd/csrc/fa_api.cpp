@@ -94,6 +94,11 @@ int fa_fwd(const FaFwdArgs *a, void *stream) {
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: q/k/v/o must be 16-byte aligned with strides multiple of 8");
     if (a->s_dmask && (a->s_rows < a->max_seqlen_q || a->s_cols < a->max_seqlen_k))
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: s_dmask extents smaller than max_seqlen");
+    // the forward addresses each sequence through 32-bit buffer offsets
+    const int64_t lim = (int64_t)1 << 31;
+    if ((int64_t)a->max_seqlen_q * a->q_row_stride * 2 >= lim || (int64_t)a->max_seqlen_k * a->k_row_stride * 2 >= lim ||
+        (int64_t)a->max_seqlen_k * a->v_row_stride * 2 >= lim)
+        return fail(FA_ERR_UNSUPPORTED, "fa_fwd: a sequence spans more than 2 GiB (seqlen * row_stride)");
     if (a->max_seqlen_q == 0) return FA_OK;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace fa {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

@@ -39,6 +39,15 @@ namespace fa {
 #ifndef FA_FWD_NW
 #define FA_FWD_NW 8        // waves per workgroup (32 query rows each)
 #endif
+#ifndef FA_FWD_MFMA_SUM
+#define FA_FWD_MFMA_SUM 0  // 1: row sums of P by an MFMA with a constant all-ones A operand
+#endif
+#ifndef FA_FWD_PKFMA
+#define FA_FWD_PKFMA 0     // 1: exponent arguments with v_pk_fma_f32 (two per instruction)
+#endif
+#ifndef FA_FWD_SETPRIO
+#define FA_FWD_SETPRIO 0   // 1: static s_setprio 1 for the second half of the waves (T5 static form)
+#endif
 #ifndef FA_FWD_WPS
 #define FA_FWD_WPS 0       // >0: __launch_bounds__ minimum waves per SIMD
 #endif
@@ -146,6 +155,7 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31;
     const int hi = lane >> 5;
+    if (FA_FWD_SETPRIO && wave >= C::NW / 2) __builtin_amdgcn_s_setprio(1);
     const int qw = q0 + 32 * wave;       // first query row of this wave
     const int qrow = qw + l32;           // the query row this lane owns
     const int head_dim = a.head_dim;
@@ -215,6 +225,9 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
         for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
     float m_i = -INFINITY;
     float l_i = 0.f;
+    f32x16 lsum;   // FA_FWD_MFMA_SUM: every register holds the running row sum of this lane's query
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lsum[r] = 0.f;
     const float c_log2 = a.softmax_scale * LOG2E;
 
     // dropout constants
@@ -302,6 +315,9 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
                 const float alpha = grow ? fast_exp2((m_i - m_new) * c_log2) : 1.f;
                 if (grow) m_i = m_new;
                 l_i *= alpha;
+                if (FA_FWD_MFMA_SUM)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
 #pragma unroll
                 for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -314,11 +330,25 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
         if constexpr (PIPE) qk(kb_rd, sn);
         {
             const float mc = (m_i == -INFINITY ? 0.f : m_i) * c_log2;
+            if (FA_FWD_PKFMA) {
+                typedef float f32x2 __attribute__((ext_vector_type(2)));
+                const f32x2 cc = {c_log2, c_log2}, mm = {-mc, -mc};
 #pragma unroll
-            for (int st = 0; st < 2; ++st)
+                for (int st = 0; st < 2; ++st)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
-            l_i += sum_tree32(s[0], s[1]);
+                    for (int r = 0; r < 16; r += 2) {
+                        f32x2 x = {s[st][r], s[st][r + 1]};
+                        x = __builtin_elementwise_fma(x, cc, mm);
+                        s[st][r] = fast_exp2(x[0]);
+                        s[st][r + 1] = fast_exp2(x[1]);
+                    }
+            } else {
+#pragma unroll
+                for (int st = 0; st < 2; ++st)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
+            }
+            if (!FA_FWD_MFMA_SUM) l_i += sum_tree32(s[0], s[1]);
 
             if (DROPOUT) {
                 // Keep mask generated in the column-major (backward) layout, transposed through a
@@ -363,6 +393,16 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
                     for (int e = 0; e < 4; ++e) pk[e] = T::pack2(s[st][8 * s2 + 2 * e], s[st][8 * s2 + 2 * e + 1]);
                     pf[st][s2] = as_frag<T>(pk);
                 }
+            if (FA_FWD_MFMA_SUM) {
+                // row sums on the matrix pipe: ones(32x16) x P^T accumulates sum_kv P into every row
+                const u32x4 ones = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};  // bf16 1.0
+                const u32x4 onesh = {0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u}; // fp16 1.0
+                const u32x4 one4 = std::is_same<T, Bf16>::value ? ones : onesh;
+#pragma unroll
+                for (int st = 0; st < 2; ++st)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) lsum = T::mfma32(as_frag<T>(one4), pf[st][s2], lsum);
+            }
             // ---- O^T += V^T P^T
 #pragma unroll
             for (int dt = 0; dt < D / 32; ++dt)
@@ -415,7 +455,7 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
     }
 
     // ---- epilogue
-    const float l_tot = pair_sum(l_i);
+    const float l_tot = FA_FWD_MFMA_SUM ? lsum[0] : pair_sum(l_i);
     const bool empty = (l_tot == 0.f) || (l_tot != l_tot);
     float inv = empty ? 1.f : 1.f / l_tot;
     if (DROPOUT) inv *= 1.0f / (1.0f - a.p_dropout);

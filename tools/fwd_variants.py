@@ -22,12 +22,12 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "pipe": {"FA_FWD_PIPE": 1},
+    "mfmasum": {"FA_FWD_MFMA_SUM": 1},
+    "pkfma": {"FA_FWD_PKFMA": 1},
+    "setprio": {"FA_FWD_SETPRIO": 1},
+    "mfmasum_pkfma": {"FA_FWD_MFMA_SUM": 1, "FA_FWD_PKFMA": 1},
+    "wps2": {"FA_FWD_WPS": 2},
     "pipe_sched": {"FA_FWD_PIPE": 1, "FA_FWD_SCHED": 1},
-    "nw8": {"FA_FWD_NW": 8},
-    "nw8_pipe": {"FA_FWD_NW": 8, "FA_FWD_PIPE": 1},
-    "wps3": {"FA_FWD_WPS": 3},
-    "nw8_wps2": {"FA_FWD_NW": 8, "FA_FWD_WPS": 2},
 }
 
 CONFIGS = [
