@@ -48,6 +48,12 @@ namespace fa {
 #ifndef FA_FWD_SETPRIO
 #define FA_FWD_SETPRIO 0   // 1: static s_setprio 1 for the second half of the waves (T5 static form)
 #endif
+#ifndef FA_FWD_PINGPONG
+#define FA_FWD_PINGPONG 0  // 1: two half-workgroups half a tile apart (matrix/VALU phases paired)
+#endif
+#ifndef FA_FWD_LDS_PAD
+#define FA_FWD_LDS_PAD 0   // extra LDS bytes per workgroup (caps workgroups per CU; experiments)
+#endif
 #ifndef FA_FWD_WPS
 #define FA_FWD_WPS 0       // >0: __launch_bounds__ minimum waves per SIMD
 #endif
@@ -63,7 +69,7 @@ struct FwdCfg {
     static constexpr int CPT = (BN * NC + NT - 1) / NT;   // staged chunks per thread per tile
     static constexpr int RNG_BYTES_PER_WAVE = 2 * 32 * 32 * 2;  // two 32x32 u16 images
     static constexpr int lds_bytes(bool dropout) {
-        return 4 * TILE_BYTES + (dropout ? NW * RNG_BYTES_PER_WAVE : 0);
+        return 4 * TILE_BYTES + (dropout ? NW * RNG_BYTES_PER_WAVE : 0) + FA_FWD_LDS_PAD;
     }
 };
 
@@ -193,26 +199,26 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
     const int k_tile_step = C::BN * (int)a.k_row_stride * 2;
     const int v_tile_step = C::BN * (int)a.v_row_stride * 2;
     u32x4 kst[C::CPT], vst[C::CPT];
-    auto gload_k = [&](int j) {
+    auto gload_k = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < C::CPT; ++i) {
             const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
             kst[i] = bload128(kr, ok ? st_off_k[i] + j * k_tile_step : OOB);
         }
     };
-    auto gload_v = [&](int j) {
+    auto gload_v = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < C::CPT; ++i) {
             const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
             vst[i] = bload128(vr, ok ? st_off_v[i] + j * v_tile_step : OOB);
         }
     };
-    auto lds_store_k = [&](char *kb) {
+    auto lds_store_k = [&](char *kb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < C::CPT; ++i)
             if ((C::BN * C::NC) % C::NT == 0 || tid + C::NT * i < C::BN * C::NC) lds_write128(kb, st_lds[i], kst[i]);
     };
-    auto lds_store_v = [&](char *vb) {
+    auto lds_store_v = [&](char *vb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < C::CPT; ++i)
             if ((C::BN * C::NC) % C::NT == 0 || tid + C::NT * i < C::BN * C::NC) lds_write128(vb, st_lds[i], vst[i]);
@@ -262,7 +268,7 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
             }
 
     // S^T = K Q^T for one 64-key tile: two 32x32 sub-tiles, lane = query row, registers = keys
-    auto qk = [&](const char *kb, f32x16 (&s)[2]) {
+    auto qk = [&](const char *kb, f32x16 (&s)[2]) __attribute__((always_inline)) {
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
 #pragma unroll
@@ -273,18 +279,168 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
         }
     };
 
-    // Software pipeline (T15): while the VALU runs the softmax of tile j, the matrix pipe
-    // computes S of tile j+1. K runs one tile ahead of V in LDS:
-    //   iteration j (parity P): reads K[j+1] from kbuf[1-P], V[j] from vbuf[P];
-    //   stages K[j+2] -> kbuf[P] and V[j+1] -> vbuf[1-P]; one barrier.
+    // ---- softmax of one tile in registers: mask, max, deferred rescale, exp, row sum,
+    // dropout, and conversion into the 16-bit B operand of P·V.
+    auto softmax_tile = [&](f32x16 (&s)[2], int kv0, typename T::frag (&pf)[2][2]) __attribute__((always_inline)) {
+        const bool need_mask = (kv0 + C::BN > seqlen_k) || (CAUSAL && kv0 + C::BN - 1 > qw);
+        if (need_mask) {
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int kv = kv0 + 32 * st + crow(r, hi);
+                    if (kv >= seqlen_k || (CAUSAL && kv > qrow)) s[st][r] = -INFINITY;
+                }
+        }
+        const float mx = pair_max(max_tree32(s[0], s[1]));
+        const float m_new = fmaxf(m_i, mx);
+        const bool grow = (m_new - m_i) * c_log2 > RESCALE_THR;   // NaN (all -inf) -> false
+        if (__builtin_amdgcn_ballot_w64(grow)) {
+            const float alpha = grow ? fast_exp2((m_i - m_new) * c_log2) : 1.f;
+            if (grow) m_i = m_new;
+            l_i *= alpha;
+            if (FA_FWD_MFMA_SUM)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        }
+        const float mc = (m_i == -INFINITY ? 0.f : m_i) * c_log2;
+        if (FA_FWD_PKFMA) {
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            const f32x2 cc = {c_log2, c_log2}, mm = {-mc, -mc};
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                    f32x2 x = {s[st][r], s[st][r + 1]};
+                    x = __builtin_elementwise_fma(x, cc, mm);
+                    s[st][r] = fast_exp2(x[0]);
+                    s[st][r + 1] = fast_exp2(x[1]);
+                }
+        } else {
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
+        }
+        if (!FA_FWD_MFMA_SUM) l_i += sum_tree32(s[0], s[1]);
+
+        if (DROPOUT) {
+            // Keep mask generated in the column-major (backward) layout, transposed through a
+            // per-wave LDS image with ds_read_b64_tr_b16.
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                char *img = rng_img + st * (32 * 32 * 2);
+                const uint32_t col = (uint32_t)(kv0 + 32 * st + l32);
+#pragma unroll
+                for (int sg = 0; sg < 2; ++sg) {
+                    const uint32_t g = ((uint32_t)(qw >> 5) << 2) | (sg << 1) | hi;
+                    u32x4 w = philox7(g, col, bh, rng_ctr3, seed_lo, seed_hi);
+                    u32x2 w01 = {w[0], w[1]}, w23 = {w[2], w[3]};
+                    lds_write64(img, l32 * 64 + (16 * sg + 4 * hi) * 2, w01);
+                    lds_write64(img, l32 * 64 + (16 * sg + 8 + 4 * hi) * 2, w23);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                char *img = rng_img + st * (32 * 32 * 2);
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    u32x2 rv = lds_read_tr(img, (8 * g4 + 4 * hi + qq) * 64 + (16 * grp + 4 * pp) * 2);
+                    const uint32_t k01 = keep2(rv[0], keep_thr), k23 = keep2(rv[1], keep_thr);
+                    if (!(k01 & 1)) s[st][4 * g4 + 0] = 0.f;
+                    if (!(k01 & 2)) s[st][4 * g4 + 1] = 0.f;
+                    if (!(k23 & 1)) s[st][4 * g4 + 2] = 0.f;
+                    if (!(k23 & 2)) s[st][4 * g4 + 3] = 0.f;
+                }
+            }
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                u32x4 pk;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) pk[e] = T::pack2(s[st][8 * s2 + 2 * e], s[st][8 * s2 + 2 * e + 1]);
+                pf[st][s2] = as_frag<T>(pk);
+            }
+    };
+
+    // ---- O^T += V^T P^T for one tile (and the optional all-ones row-sum MFMA)
+    auto pv = [&](const char *vb, typename T::frag (&pf)[2][2]) __attribute__((always_inline)) {
+        if (FA_FWD_MFMA_SUM) {
+            const u32x4 ones = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};  // bf16 1.0
+            const u32x4 onesh = {0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u}; // fp16 1.0
+            const u32x4 one4 = std::is_same<T, Bf16>::value ? ones : onesh;
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) lsum = T::mfma32(as_frag<T>(one4), pf[st][s2], lsum);
+        }
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    u32x2 lo = lds_read_tr(vb, v_rd[dt][st][s2][0]);
+                    u32x2 hv = lds_read_tr(vb, v_rd[dt][st][s2][1]);
+                    u32x4 av = {lo[0], lo[1], hv[0], hv[1]};
+                    o[dt] = T::mfma32(as_frag<T>(av), pf[st][s2], o[dt]);
+                }
+    };
+
+#if FA_FWD_PINGPONG
+    // ---- Ping-pong (two barriers per tile). Waves 0..NW/2-1 ("A") and NW/2..NW-1 ("B") share
+    // every SIMD pairwise and run half a tile apart, so each phase pairs one wave's matrix work
+    // with its partner's softmax:
+    //   iteration j, phase 1:  A: P·V(j-1), S(j) = K(j)Q^T   |  B: softmax(j-1)
+    //   iteration j, phase 2:  A: softmax(j)                  |  B: P·V(j-1), S(j)
+    // LDS: iteration j reads K(j) from kbuf[j&1] and V(j-1) from vbuf[(j-1)&1], and stages
+    // K(j+1) -> kbuf[(j+1)&1], V(j) -> vbuf[j&1] (both last read in iteration j-1).
+    {
+        const bool half_b = wave >= C::NW / 2;
+        f32x16 s[2];
+        typename T::frag pf[2][2];
+        auto mfma_phase = [&](auto par_tag, int j) __attribute__((always_inline)) {
+            constexpr int P = decltype(par_tag)::value;   // parity of j
+            if (j >= 1) pv(smem + (2 + (1 - P)) * C::TILE_BYTES, pf);
+            if (j < nt) qk(smem + P * C::TILE_BYTES, s);
+        };
+        auto iter = [&](auto par_tag, int j) __attribute__((always_inline)) {
+            constexpr int P = decltype(par_tag)::value;
+            gload_k(j + 1);
+            gload_v(j);
+            if (!half_b) mfma_phase(par_tag, j);
+            else if (j >= 1) softmax_tile(s, (j - 1) * C::BN, pf);
+            __syncthreads();
+            if (!half_b) { if (j < nt) softmax_tile(s, j * C::BN, pf); }
+            else mfma_phase(par_tag, j);
+            lds_store_k(smem + (1 - P) * C::TILE_BYTES);
+            lds_store_v(smem + (2 + P) * C::TILE_BYTES);
+            __syncthreads();
+        };
+        gload_k(0);
+        lds_store_k(smem);
+        __syncthreads();
+        for (int j = 0; j <= nt; j += 2) {
+            iter(std::integral_constant<int, 0>(), j);
+            if (j + 1 <= nt) iter(std::integral_constant<int, 1>(), j + 1);
+        }
+    }
+#else
+    // Software pipeline (T15, FA_FWD_PIPE): while the VALU runs the softmax of tile j, the matrix
+    // pipe computes S of tile j+1 (K one tile ahead of V in LDS). Plain: K[j], V[j] in buffer P.
     f32x16 sA[2], sB[2];   // S of even / odd tiles
-    auto step = [&](auto par_tag, int j) {
+    auto step = [&](auto par_tag, int j) __attribute__((always_inline)) {
         constexpr int P = decltype(par_tag)::value;
+        constexpr bool PIPE = FA_FWD_PIPE;
         f32x16 (&s)[2] = P == 0 ? sA : sB;       // this tile's scores
         f32x16 (&sn)[2] = P == 0 ? sB : sA;      // next tile's scores
-        constexpr bool PIPE = FA_FWD_PIPE;
-        // pipelined: K one tile ahead (read K[j+1] from kbuf[1-P], stage K[j+2] into kbuf[P]);
-        // plain: K[j], V[j] in buffer P, stage tile j+1 into buffer 1-P.
         char *kb_rd = smem + (PIPE ? 1 - P : P) * C::TILE_BYTES;
         char *vb_rd = smem + (2 + P) * C::TILE_BYTES;
         char *kb_wr = smem + (PIPE ? P : 1 - P) * C::TILE_BYTES;
@@ -293,146 +449,13 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
         gload_k(PIPE ? j + 2 : j + 1);
         gload_v(j + 1);
         if constexpr (!PIPE) qk(kb_rd, s);
-
-        {
-            // ---- mask (only on the ragged last tile and the causal diagonal; a tile entirely
-            // above the diagonal for this wave comes out all -inf, i.e. contributes zeros)
-            const bool need_mask = (kv0 + C::BN > seqlen_k) || (CAUSAL && kv0 + C::BN - 1 > qw);
-            if (need_mask) {
-#pragma unroll
-                for (int st = 0; st < 2; ++st)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int kv = kv0 + 32 * st + crow(r, hi);
-                        if (kv >= seqlen_k || (CAUSAL && kv > qrow)) s[st][r] = -INFINITY;
-                    }
-            }
-            // ---- online softmax with deferred rescale
-            const float mx = pair_max(max_tree32(s[0], s[1]));
-            const float m_new = fmaxf(m_i, mx);
-            const bool grow = (m_new - m_i) * c_log2 > RESCALE_THR;   // NaN (all -inf) -> false
-            if (__builtin_amdgcn_ballot_w64(grow)) {
-                const float alpha = grow ? fast_exp2((m_i - m_new) * c_log2) : 1.f;
-                if (grow) m_i = m_new;
-                l_i *= alpha;
-                if (FA_FWD_MFMA_SUM)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
-#pragma unroll
-                for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-            }
+        typename T::frag pf[2][2];
+        if constexpr (PIPE) {
+            // split the softmax so the next tile's MFMAs overlap its exp/sum part
+            qk(kb_rd, sn);
         }
-        // ---- branch-free from here to the barrier (one scheduling region): the next tile's
-        // scores on the matrix pipe interleaved with this tile's exp/sum/convert on the VALU.
-        // Inactive (fully masked) tiles compute zeros: their scores are -inf.
-        if constexpr (PIPE) qk(kb_rd, sn);
-        {
-            const float mc = (m_i == -INFINITY ? 0.f : m_i) * c_log2;
-            if (FA_FWD_PKFMA) {
-                typedef float f32x2 __attribute__((ext_vector_type(2)));
-                const f32x2 cc = {c_log2, c_log2}, mm = {-mc, -mc};
-#pragma unroll
-                for (int st = 0; st < 2; ++st)
-#pragma unroll
-                    for (int r = 0; r < 16; r += 2) {
-                        f32x2 x = {s[st][r], s[st][r + 1]};
-                        x = __builtin_elementwise_fma(x, cc, mm);
-                        s[st][r] = fast_exp2(x[0]);
-                        s[st][r + 1] = fast_exp2(x[1]);
-                    }
-            } else {
-#pragma unroll
-                for (int st = 0; st < 2; ++st)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
-            }
-            if (!FA_FWD_MFMA_SUM) l_i += sum_tree32(s[0], s[1]);
-
-            if (DROPOUT) {
-                // Keep mask generated in the column-major (backward) layout, transposed through a
-                // per-wave LDS image with ds_read_b64_tr_b16.
-#pragma unroll
-                for (int st = 0; st < 2; ++st) {
-                    char *img = rng_img + st * (32 * 32 * 2);
-                    const uint32_t col = (uint32_t)(kv0 + 32 * st + l32);
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg) {
-                        const uint32_t g = ((uint32_t)(qw >> 5) << 2) | (sg << 1) | hi;
-                        u32x4 w = philox7(g, col, bh, rng_ctr3, seed_lo, seed_hi);
-                        u32x2 w01 = {w[0], w[1]}, w23 = {w[2], w[3]};
-                        lds_write64(img, l32 * 64 + (16 * sg + 4 * hi) * 2, w01);
-                        lds_write64(img, l32 * 64 + (16 * sg + 8 + 4 * hi) * 2, w23);
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-#pragma unroll
-                for (int st = 0; st < 2; ++st) {
-                    char *img = rng_img + st * (32 * 32 * 2);
-#pragma unroll
-                    for (int g4 = 0; g4 < 4; ++g4) {
-                        u32x2 rv = lds_read_tr(img, (8 * g4 + 4 * hi + qq) * 64 + (16 * grp + 4 * pp) * 2);
-                        const uint32_t k01 = keep2(rv[0], keep_thr), k23 = keep2(rv[1], keep_thr);
-                        if (!(k01 & 1)) s[st][4 * g4 + 0] = 0.f;
-                        if (!(k01 & 2)) s[st][4 * g4 + 1] = 0.f;
-                        if (!(k23 & 1)) s[st][4 * g4 + 2] = 0.f;
-                        if (!(k23 & 2)) s[st][4 * g4 + 3] = 0.f;
-                    }
-                }
-            }
-
-            // ---- P (16-bit) as the B operand: registers 8s2..8s2+7 of sub-tile st
-            typename T::frag pf[2][2];
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    u32x4 pk;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) pk[e] = T::pack2(s[st][8 * s2 + 2 * e], s[st][8 * s2 + 2 * e + 1]);
-                    pf[st][s2] = as_frag<T>(pk);
-                }
-            if (FA_FWD_MFMA_SUM) {
-                // row sums on the matrix pipe: ones(32x16) x P^T accumulates sum_kv P into every row
-                const u32x4 ones = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};  // bf16 1.0
-                const u32x4 onesh = {0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u}; // fp16 1.0
-                const u32x4 one4 = std::is_same<T, Bf16>::value ? ones : onesh;
-#pragma unroll
-                for (int st = 0; st < 2; ++st)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) lsum = T::mfma32(as_frag<T>(one4), pf[st][s2], lsum);
-            }
-            // ---- O^T += V^T P^T
-#pragma unroll
-            for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-                for (int st = 0; st < 2; ++st)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) {
-                        u32x2 lo = lds_read_tr(vb_rd, v_rd[dt][st][s2][0]);
-                        u32x2 hv = lds_read_tr(vb_rd, v_rd[dt][st][s2][1]);
-                        u32x4 av = {lo[0], lo[1], hv[0], hv[1]};
-                        o[dt] = T::mfma32(as_frag<T>(av), pf[st][s2], o[dt]);
-                    }
-        }
-        if constexpr (!DROPOUT && FA_FWD_SCHED && PIPE) {
-            // pin the interleave (T19): all next-tile K reads first; then per next-tile MFMA two
-            // V^T transposed reads and ~10 softmax VALU ops; then the P·V MFMAs with the rest.
-            constexpr int NQK = 2 * (D / 16), NPV = 4 * (D / 32);
-            __builtin_amdgcn_sched_group_barrier(0x100, NQK, 0);
-#pragma unroll
-            for (int i = 0; i < NQK; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, (2 * NPV) / NQK, 0);
-                __builtin_amdgcn_sched_group_barrier(0x402, 88 / NQK, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < NPV; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x402, 4, 0);
-            }
-        }
+        softmax_tile(s, kv0, pf);
+        pv(vb_rd, pf);
         lds_store_k(kb_wr);
         lds_store_v(vb_wr);
         __syncthreads();
@@ -453,6 +476,7 @@ __global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
         step(std::integral_constant<int, 0>(), j);
         if (j + 1 < nt) step(std::integral_constant<int, 1>(), j + 1);
     }
+#endif
 
     // ---- epilogue
     const float l_tot = FA_FWD_MFMA_SUM ? lsum[0] : pair_sum(l_i);

@@ -22,12 +22,10 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "mfmasum": {"FA_FWD_MFMA_SUM": 1},
-    "pkfma": {"FA_FWD_PKFMA": 1},
-    "setprio": {"FA_FWD_SETPRIO": 1},
-    "mfmasum_pkfma": {"FA_FWD_MFMA_SUM": 1, "FA_FWD_PKFMA": 1},
-    "wps2": {"FA_FWD_WPS": 2},
-    "pipe_sched": {"FA_FWD_PIPE": 1, "FA_FWD_SCHED": 1},
+    "pingpong": {"FA_FWD_PINGPONG": 1},
+    "pingpong_setprio": {"FA_FWD_PINGPONG": 1, "FA_FWD_SETPRIO": 1},
+    "pingpong_1wg": {"FA_FWD_PINGPONG": 1, "FA_FWD_LDS_PAD": 96 * 1024},
+    "pingpong_mfmasum": {"FA_FWD_PINGPONG": 1, "FA_FWD_MFMA_SUM": 1},
 }
 
 CONFIGS = [
