@@ -23,11 +23,11 @@ hipError_t launch_probs(const FaFwdArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t s) {
-    dim3 grid((a.max_seqlen_q + 63) / 64, a.nheads, a.batch);
+    dim3 grid((a.max_seqlen_q + 15) / 16, a.nheads, a.batch);
     if (a.dtype == FA_DTYPE_BF16)
-        hipLaunchKernelGGL(fa_bwd_dot_kernel<Bf16>, grid, dim3(64), 0, s, a);
+        hipLaunchKernelGGL(fa_bwd_dot_kernel<Bf16>, grid, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(fa_bwd_dot_kernel<Fp16>, grid, dim3(64), 0, s, a);
+        hipLaunchKernelGGL(fa_bwd_dot_kernel<Fp16>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

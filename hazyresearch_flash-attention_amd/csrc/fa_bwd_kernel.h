@@ -24,9 +24,15 @@
 
 namespace fa {
 
-template <int D>
+// Waves per workgroup (32 keys each). dQ atomic bytes scale with 1/NW, so non-causal uses 8;
+// causal uses 4: smaller key blocks balance the triangular work better.
+template <bool CAUSAL>
+struct BwdWaves { static constexpr int value = CAUSAL ? 4 : 8; };
+
+template <int D, int NW_ = 8>
 struct BwdCfg {
-    static constexpr int NW = 4;
+    static constexpr int NW = NW_;
+    static constexpr int NT = 64 * NW;      // threads per workgroup
     static constexpr int BKV = 32 * NW;     // keys per workgroup
     static constexpr int BQ = 32;           // query rows per iteration
     static constexpr int NC = D / 8;
@@ -34,43 +40,51 @@ struct BwdCfg {
     static constexpr int Q_IMG = BQ * D * 2;
     static constexpr int DS_IMG = BKV * BQ * 2;
     static constexpr int OFF_K = 0;
-    static constexpr int OFF_Q = OFF_K + K_IMG;
-    static constexpr int OFF_DO = OFF_Q + Q_IMG;
-    static constexpr int OFF_DS = OFF_DO + Q_IMG;
-    static constexpr int OFF_LSE = OFF_DS + DS_IMG;
-    static constexpr int OFF_DELTA = OFF_LSE + BQ * 4;
-    static constexpr int LDS_BYTES = OFF_DELTA + BQ * 4;
+    static constexpr int OFF_Q = OFF_K + K_IMG;          // Q[2]  (double-buffered query tiles)
+    static constexpr int OFF_DO = OFF_Q + 2 * Q_IMG;     // dO[2]
+    static constexpr int OFF_DS = OFF_DO + 2 * Q_IMG;
+    static constexpr int OFF_LSE = OFF_DS + DS_IMG;      // lse[2][BQ]
+    static constexpr int OFF_DELTA = OFF_LSE + 2 * BQ * 4;
+    static constexpr int LDS_BYTES = OFF_DELTA + 2 * BQ * 4;
+    static constexpr int QCH = (BQ * NC + NT - 1) / NT;   // staged 16-B chunks per thread per tile
 };
 
 // byte offset in the dS^T image ([key][query], 64-B rows) of query column q (multiple of 4) of
-// key row r. The 32-B half is flipped on rows with bit 3 set so that the dQ transposed reads
-// (two 4-row blocks 8 rows apart per half-wave) are bank-conflict free.
-__device__ __forceinline__ int ds_off(int r, int q) { return r * 64 + ((q * 2) ^ (((r >> 3) & 1) << 5)); }
+// key row r. The 8-B slot is XOR-ed with (r>>1)&7 so that both the ds_write_b64 of a 16-lane
+// group (16 consecutive rows, one column) and the dQ transposed reads (two 4-row blocks 8 rows
+// apart per half-wave) touch every bank once.
+__device__ __forceinline__ int ds_off(int r, int q) { return r * 64 + ((q * 2) ^ (((r >> 1) & 7) << 3)); }
 
-// delta = rowsum(dO * O) (softmax_d), and zero the fp32 dQ accumulator.
+// delta = rowsum(dO * O) (softmax_d), and zero the fp32 dQ accumulator. 16 threads per row
+// (one 16-B chunk each), 16 rows per 256-thread block, shuffle reduction over the 16 lanes.
 template <typename T>
-__global__ __launch_bounds__(64) void fa_bwd_dot_kernel(const FaBwdArgs a) {
+__global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const FaBwdArgs a) {
     const int b = blockIdx.z, h = blockIdx.y;
     const int q_start = a.cu_seqlens_q[b];
     const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
-    const int row = blockIdx.x * 64 + threadIdx.x;
-    if (row >= seqlen_q) return;
-    const uint16_t *dop = (const uint16_t *)a.dout + (int64_t)(q_start + row) * a.do_row_stride + (int64_t)h * a.do_head_stride;
-    const uint16_t *op = (const uint16_t *)a.out + (int64_t)(q_start + row) * a.o_row_stride + (int64_t)h * a.o_head_stride;
-    float *acc = a.dq_accum + ((int64_t)(q_start + row) * a.nheads + h) * a.head_dim;
+    const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int c = threadIdx.x & 15;
+    const bool ok = row < seqlen_q && c * 8 < a.head_dim;
     float sum = 0.f;
-    for (int c = 0; c < a.head_dim; c += 8) {
-        u32x4 x = gload128(dop + c), y = gload128(op + c);
+    if (ok) {
+        const uint16_t *dop = (const uint16_t *)a.dout + (int64_t)(q_start + row) * a.do_row_stride +
+                              (int64_t)h * a.do_head_stride + c * 8;
+        const uint16_t *op = (const uint16_t *)a.out + (int64_t)(q_start + row) * a.o_row_stride +
+                             (int64_t)h * a.o_head_stride + c * 8;
+        const u32x4 x = gload128(dop), y = gload128(op);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             sum += T::to_float(x[e] & 0xFFFF) * T::to_float(y[e] & 0xFFFF);
             sum += T::to_float(x[e] >> 16) * T::to_float(y[e] >> 16);
         }
-        f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<f32x4 *>(acc + c) = z;
-        *reinterpret_cast<f32x4 *>(acc + c + 4) = z;
+        float *acc = a.dq_accum + ((int64_t)(q_start + row) * a.nheads + h) * a.head_dim + c * 8;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4 *>(acc) = z;
+        *reinterpret_cast<f32x4 *>(acc + 4) = z;
     }
-    a.softmax_d[(int64_t)(b * a.nheads + h) * a.lse_stride + row] = sum;
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1) sum += __shfl_xor(sum, w, 16);
+    if (c == 0 && row < seqlen_q) a.softmax_d[(int64_t)(b * a.nheads + h) * a.lse_stride + row] = sum;
 }
 
 // dq = scale * dq_accum, converted to 16-bit into the (possibly strided) dq.
@@ -93,25 +107,40 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
     gstore128((uint16_t *)a.dq + row * a.dq_row_stride + h * a.dq_head_stride + c * 8, w);
 }
 
+#ifndef FA_BWD_MINW
+#define FA_BWD_MINW 2   // __launch_bounds__ minimum waves per SIMD (2: two workgroups per CU when causal)
+#endif
+#if FA_BWD_MINW > 0
+#define FA_BWD_BOUNDS(C) __launch_bounds__(64 * BwdWaves<C>::value, FA_BWD_MINW)
+#else
+#define FA_BWD_BOUNDS(C) __launch_bounds__(64 * BwdWaves<C>::value)
+#endif
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
-__global__ __launch_bounds__(256) void fa_bwd_kernel(const FaBwdArgs a) {
-    using C = BwdCfg<D>;
+__global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a) {
+    using C = BwdCfg<D, BwdWaves<CAUSAL>::value>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char *kimg = smem + C::OFF_K;
-    char *qimg = smem + C::OFF_Q;
-    char *doimg = smem + C::OFF_DO;
     char *dsimg = smem + C::OFF_DS;
     float *lse_s = (float *)(smem + C::OFF_LSE);
     float *del_s = (float *)(smem + C::OFF_DELTA);
 
-    const int b = blockIdx.z, h = blockIdx.y;
+    // causal: key block kb sees queries kb*BKV..end, so block 0 is the heaviest: launch all
+    // heads' block 0 first, then block 1, ... (LPT order)
+    int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    if (CAUSAL) {
+        const int nbh = gridDim.y * gridDim.z;
+        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        kb = L / nbh;
+        h = (L % nbh) % gridDim.y;
+        b = (L % nbh) / gridDim.y;
+    }
     const int q_start = a.cu_seqlens_q[b];
     const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
     const int k_start = a.cu_seqlens_k[b];
     const int seqlen_k = a.cu_seqlens_k[b + 1] - k_start;
-    const int k0 = blockIdx.x * C::BKV;
+    const int k0 = kb * C::BKV;
     if (k0 >= seqlen_k) return;
 
     const int tid = threadIdx.x;
@@ -133,7 +162,7 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const FaBwdArgs a) {
     const int64_t dqa_row = (int64_t)a.nheads * head_dim;
 
     // ---- stage the K block image (B operand of dQ = dS K, transposed reads)
-    for (int idx = tid; idx < C::BKV * C::NC; idx += 256) {
+    for (int idx = tid; idx < C::BKV * C::NC; idx += C::NT) {
         const int row = idx / C::NC, c = idx % C::NC;
         const int kv = k0 + row;
         u32x4 v = {0u, 0u, 0u, 0u};
@@ -175,31 +204,57 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const FaBwdArgs a) {
     const int q_begin = CAUSAL ? k0 : 0;   // rows q < k0 see no key of this block
     const int nqt = seqlen_q > q_begin ? (seqlen_q - q_begin + C::BQ - 1) / C::BQ : 0;
 
-    for (int it = 0; it < nqt; ++it) {
-        const int q0 = q_begin + it * C::BQ;
-        // ---- stage Q, dO tiles, lse (pre-multiplied by log2 e) and delta
-        for (int idx = tid; idx < C::BQ * C::NC; idx += 256) {
+    // ---- query-tile staging: issue the next tile's loads early, write them late (T14), into
+    // the other half of the double-buffered Q/dO/lse/delta images.
+    u32x4 qst[C::QCH], dst[C::QCH];
+    float lse_st = 0.f, del_st = 0.f;
+    auto gload_qtile = [&](int q0n) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < C::QCH; ++i) {
+            const int idx = tid + C::NT * i;
             const int row = idx / C::NC, c = idx % C::NC;
-            const int q = q0 + row;
-            u32x4 x = {0u, 0u, 0u, 0u}, y = {0u, 0u, 0u, 0u};
-            if (q < seqlen_q && c * 8 < head_dim) {
-                x = gload128(qp + (int64_t)q * a.q_row_stride + c * 8);
-                y = gload128(dop + (int64_t)q * a.do_row_stride + c * 8);
-            }
-            lds_write128(qimg, S::off(row, c), x);
-            lds_write128(doimg, S::off(row, c), y);
+            const int q = q0n + row;
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            const bool ok = idx < C::BQ * C::NC && q < seqlen_q && c * 8 < head_dim;
+            qst[i] = ok ? gload128(qp + (int64_t)q * a.q_row_stride + c * 8) : z;
+            dst[i] = ok ? gload128(dop + (int64_t)q * a.do_row_stride + c * 8) : z;
         }
         if (tid < C::BQ) {
-            const int q = q0 + tid;
-            lse_s[tid] = q < seqlen_q ? lse_g[q] * LOG2E : 0.f;
-            del_s[tid] = q < seqlen_q ? del_g[q] : 0.f;
+            const int q = q0n + tid;
+            lse_st = q < seqlen_q ? lse_g[q] * LOG2E : 0.f;
+            del_st = q < seqlen_q ? del_g[q] : 0.f;
         }
-        __syncthreads();
-
-        const bool active = !CAUSAL || (q0 + C::BQ - 1 >= kw);
-        f32x16 ds;
+    };
+    auto lds_store_qtile = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ds[r] = 0.f;
+        for (int i = 0; i < C::QCH; ++i) {
+            const int idx = tid + C::NT * i;
+            if ((C::BQ * C::NC) % C::NT == 0 || idx < C::BQ * C::NC) {
+                const int row = idx / C::NC, c = idx % C::NC;
+                lds_write128(smem + C::OFF_Q + buf * C::Q_IMG, S::off(row, c), qst[i]);
+                lds_write128(smem + C::OFF_DO + buf * C::Q_IMG, S::off(row, c), dst[i]);
+            }
+        }
+        if (tid < C::BQ) {
+            lse_s[buf * C::BQ + tid] = lse_st;
+            del_s[buf * C::BQ + tid] = del_st;
+        }
+    };
+    if (nqt > 0) {
+        gload_qtile(q_begin);
+        lds_store_qtile(0);
+    }
+    __syncthreads();
+
+    auto qstep = [&](auto par_tag, int it) __attribute__((always_inline)) {
+        constexpr int BUF = decltype(par_tag)::value;
+        char *qimg = smem + C::OFF_Q + BUF * C::Q_IMG;
+        char *doimg = smem + C::OFF_DO + BUF * C::Q_IMG;
+        const float *lse_b = lse_s + BUF * C::BQ;
+        const float *del_b = del_s + BUF * C::BQ;
+        const int q0 = q_begin + it * C::BQ;
+        if (it + 1 < nqt) gload_qtile(q0 + C::BQ);
+        const bool active = !CAUSAL || (q0 + C::BQ - 1 >= kw);
         if (active) {
             // ---- S = Q K^T and dZ = dO V^T : lane = key, registers = query rows crow(r,hi)
             f32x16 sacc, zacc;
@@ -213,12 +268,6 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const FaBwdArgs a) {
                 zacc = T::mfma32(as_frag<T>(da), vf[ks], zacc);
             }
             // row constants for rows crow(4g+e, hi) = 8g + 4hi + e (16-B aligned groups of 4)
-            f32x4 lse4[4], del4[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                lse4[g] = *reinterpret_cast<const f32x4 *>(lse_s + 8 * g + 4 * hi);
-                del4[g] = *reinterpret_cast<const f32x4 *>(del_s + 8 * g + 4 * hi);
-            }
             const bool need_mask = (q0 + C::BQ > seqlen_q) || (k0 + C::BKV > seqlen_k) ||
                                    (CAUSAL && q0 < kw + 31);
             u32x4 rw[2];
@@ -229,29 +278,36 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const FaBwdArgs a) {
                     rw[sg] = philox7(g, (uint32_t)kvrow, bh, rng_ctr3, seed_lo, seed_hi);
                 }
             }
-            f32x16 pd;
+            // P and dS in place: sacc -> Pd (dropped, scaled P), zacc -> dS. Row constants for
+            // rows crow(4g+e, hi) = 8g + 4hi + e are one 16-B LDS read per group of 4 registers.
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float lse2 = lse4[r >> 2][r & 3];
-                const float del = del4[r >> 2][r & 3];
-                float p = fast_exp2(fmaf(sacc[r], c_log2, -lse2));
-                if (need_mask) {
-                    const int q = q0 + crow(r, hi);
-                    if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 lse4 = *reinterpret_cast<const f32x4 *>(lse_b + 8 * g + 4 * hi);
+                const f32x4 del4 = *reinterpret_cast<const f32x4 *>(del_b + 8 * g + 4 * hi);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 4 * g + e;
+                    float p = fast_exp2(fmaf(sacc[r], c_log2, -lse4[e]));
+                    if (need_mask) {
+                        const int q = q0 + crow(r, hi);
+                        if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
+                    }
+                    float dpv = zacc[r];
+                    float pdv = p;
+                    if (DROPOUT) {
+                        const int slot = (r & 3) | (((r >> 2) & 1) << 2);
+                        const uint32_t word = rw[r >> 3][slot >> 1];
+                        const uint32_t rnd = (slot & 1) ? (word >> 16) : (word & 0xFFFFu);
+                        const bool keep = rnd <= keep_thr;
+                        dpv = keep ? dpv * rp : 0.f;
+                        pdv = keep ? p * rp : 0.f;
+                    }
+                    sacc[r] = pdv;
+                    zacc[r] = p * (dpv - del4[e]);
                 }
-                float dpv = zacc[r];
-                float pdv = p;
-                if (DROPOUT) {
-                    const int slot = (r & 3) | (((r >> 2) & 1) << 2);
-                    const uint32_t word = rw[r >> 3][slot >> 1];
-                    const uint32_t rnd = (slot & 1) ? (word >> 16) : (word & 0xFFFFu);
-                    const bool keep = rnd <= keep_thr;
-                    dpv = keep ? dpv * rp : 0.f;
-                    pdv = keep ? p * rp : 0.f;
-                }
-                pd[r] = pdv;
-                ds[r] = p * (dpv - del);
             }
+            f32x16 &pd = sacc;
+            f32x16 &ds = zacc;
             // ---- dV^T += dO^T Pd ; dK^T += Q^T dS  (A operands by transposed reads)
 #pragma unroll
             for (int sg = 0; sg < 2; ++sg) {
@@ -275,21 +331,29 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const FaBwdArgs a) {
                     dk[dt] = T::mfma32(as_frag<T>(bv), as_frag<T>(sk), dk[dt]);
                 }
             }
-        }
-        // ---- dS^T image: row = key (32*wave + l32), columns = query rows 8g + 4hi .. +3
+            // ---- dS^T image: row = key (32*wave + l32), columns = query rows 8g + 4hi .. +3
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            u32x2 w = {T::pack2(ds[4 * g + 0], ds[4 * g + 1]), T::pack2(ds[4 * g + 2], ds[4 * g + 3])};
-            lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), w);
+            for (int g = 0; g < 4; ++g) {
+                u32x2 w = {T::pack2(ds[4 * g + 0], ds[4 * g + 1]), T::pack2(ds[4 * g + 2], ds[4 * g + 3])};
+                lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), w);
+            }
+        } else {
+            // keys of this wave are all above the causal diagonal for this query tile: dS = 0
+            const u32x2 z = {0u, 0u};
+#pragma unroll
+            for (int g = 0; g < 4; ++g) lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), z);
         }
         __syncthreads();
 
-        // ---- dQ[q][d] += dS[q][key] K[key][d] over the 128 keys (16x16x32 MFMAs)
-        {
-            const int qh = wave & 1;
+        // ---- dQ[q][d] += dS[q][key] K[key][d] over the BKV keys (16x16x32 MFMAs); the
+        // 2*(D/16) output tiles of 16 query rows x 16 columns are dealt round-robin to the waves,
+        // each summing over every key of the block, so one fp32 atomic per element per block.
 #pragma unroll
-            for (int t = 0; t < D / 32; ++t) {
-                const int dbase = 16 * ((wave >> 1) + 2 * t);
+        for (int t0 = 0; t0 < 2 * (D / 16); t0 += C::NW) {
+            const int t = t0 + wave;
+            if (t < 2 * (D / 16)) {
+                const int qh = t & 1;
+                const int dbase = 16 * (t >> 1);
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int ks = 0; ks < C::BKV / 32; ++ks) {
@@ -312,7 +376,12 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const FaBwdArgs a) {
                 }
             }
         }
+        if (it + 1 < nqt) lds_store_qtile(1 - BUF);
         __syncthreads();
+    };
+    for (int it = 0; it < nqt; it += 2) {
+        qstep(std::integral_constant<int, 0>(), it);
+        if (it + 1 < nqt) qstep(std::integral_constant<int, 1>(), it + 1);
     }
 
     // ---- epilogue: dV, dK (scaled) rows of this lane's key

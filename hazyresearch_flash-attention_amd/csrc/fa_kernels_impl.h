@@ -21,13 +21,13 @@ static hipError_t launch_fwd_t(const FaFwdArgs &a, hipStream_t stream) {
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
 static hipError_t launch_bwd_t(const FaBwdArgs &a, hipStream_t stream) {
-    using C = BwdCfg<D>;
+    using C = BwdCfg<D, BwdWaves<CAUSAL>::value>;
     auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT>;
     static const hipError_t attr_err =
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
     if (attr_err != hipSuccess) return attr_err;
     dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(256), C::LDS_BYTES, stream, a);
+    hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a);
     return hipGetLastError();
 }
 
