@@ -36,9 +36,6 @@ namespace fa {
 #ifndef FA_FWD_SCHED
 #define FA_FWD_SCHED 0     // 1: pin the MFMA/VALU interleave with sched_group_barrier (T19)
 #endif
-#ifndef FA_FWD_NW
-#define FA_FWD_NW 8        // waves per workgroup (32 query rows each)
-#endif
 #ifndef FA_FWD_MFMA_SUM
 #define FA_FWD_MFMA_SUM 0  // 1: row sums of P by an MFMA with a constant all-ones A operand
 #endif
@@ -58,9 +55,10 @@ namespace fa {
 #define FA_FWD_WPS 0       // >0: __launch_bounds__ minimum waves per SIMD
 #endif
 
-template <int D>
+// NW = waves per workgroup (32 query rows each); chosen per launch (fa_kernels_impl.h).
+template <int D, int NW_>
 struct FwdCfg {
-    static constexpr int NW = FA_FWD_NW;          // waves per workgroup
+    static constexpr int NW = NW_;                // waves per workgroup
     static constexpr int NT = 64 * NW;            // threads per workgroup
     static constexpr int BM = 32 * NW;            // query rows per workgroup
     static constexpr int BN = 64;                 // keys per iteration
@@ -116,14 +114,14 @@ __device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
 }
 
 #if FA_FWD_WPS > 0
-#define FA_FWD_BOUNDS __launch_bounds__(64 * FA_FWD_NW, FA_FWD_WPS)
+#define FA_FWD_BOUNDS(NW) __launch_bounds__(64 * NW, FA_FWD_WPS)
 #else
-#define FA_FWD_BOUNDS __launch_bounds__(64 * FA_FWD_NW)
+#define FA_FWD_BOUNDS(NW) __launch_bounds__(64 * NW)
 #endif
 
-template <int D, typename T, bool CAUSAL, bool DROPOUT>
-__global__ FA_FWD_BOUNDS void fa_fwd_kernel(const FaFwdArgs a) {
-    using C = FwdCfg<D>;
+template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW>
+__global__ FA_FWD_BOUNDS(NW) void fa_fwd_kernel(const FaFwdArgs a) {
+    using C = FwdCfg<D, NW>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];

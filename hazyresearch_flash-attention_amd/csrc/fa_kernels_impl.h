@@ -4,19 +4,41 @@
 #include "fa_fwd_kernel.h"
 #include "fa_bwd_kernel.h"
 
+#include <cstdlib>
+
 namespace fa {
 
-template <int D, typename T, bool CAUSAL, bool DROPOUT>
-static hipError_t launch_fwd_t(const FaFwdArgs &a, hipStream_t stream) {
-    using C = FwdCfg<D>;
+template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW>
+static hipError_t launch_fwd_nw(const FaFwdArgs &a, hipStream_t stream) {
+    using C = FwdCfg<D, NW>;
     const int lds = C::lds_bytes(DROPOUT);
-    auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT>;
+    auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT, NW>;
     static const hipError_t attr_err =
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (attr_err != hipSuccess) return attr_err;
     dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
     hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a);
     return hipGetLastError();
+}
+
+// Waves per workgroup. 8 (256 query rows) measured fastest on every BASELINE config, including
+// the short S=512 one where fewer waves would spread over more CUs (344 vs 339 vs 331 TF/s for
+// 8/4/2). FA_FWD_NW=2|4|8 overrides it for tuning.
+static int pick_fwd_waves(const FaFwdArgs &) {
+    static const int forced = [] {
+        const char *e = getenv("FA_FWD_NW");
+        return e ? atoi(e) : 0;
+    }();
+    return (forced == 2 || forced == 4) ? forced : 8;
+}
+
+template <int D, typename T, bool CAUSAL, bool DROPOUT>
+static hipError_t launch_fwd_t(const FaFwdArgs &a, hipStream_t stream) {
+    switch (pick_fwd_waves(a)) {
+        case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, stream);
+        case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, stream);
+        default: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 2>(a, stream);
+    }
 }
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
