@@ -42,8 +42,9 @@ class RotaryEmbedding(torch.nn.Module):
         if (seq_len != self._seq_len_cached or self._cos_cached.device != x.device
                 or self._cos_cached.dtype != x.dtype):
             self._seq_len_cached = seq_len
-            t = torch.arange(seq_len, device=x.device, dtype=self.inv_freq.dtype)
-            freqs = torch.outer(t, self.inv_freq)
+            inv_freq = self.inv_freq.to(x.device)   # FlashMHA(device=...) leaves the buffer on cpu
+            t = torch.arange(seq_len, device=x.device, dtype=inv_freq.dtype)
+            freqs = torch.outer(t, inv_freq)
             self._cos_cached = torch.cos(freqs).to(x.dtype).repeat_interleave(2, dim=-1)
             self._sin_cached = torch.sin(freqs).to(x.dtype).repeat_interleave(2, dim=-1)
         return self._cos_cached, self._sin_cached
