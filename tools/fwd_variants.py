@@ -4,7 +4,7 @@
     python tools/fwd_variants.py run [--rounds 5]  # on the GPU box: time every variant, interleaved
 
 Each variant recompiles only the head-dim TUs with its -D switches (FA_FWD_PIPE, FA_FWD_SCHED,
-FA_FWD_NW, FA_FWD_WPS) and links them with the shared objects of the main build. The run
+FA_FWD_WPS, ...; a key starting with '-' is passed as a raw compiler flag) and links them with the shared objects of the main build. The run
 loads each library with ctypes (RTLD_LOCAL) and calls fa_fwd on the same device tensors.
 """
 import argparse
@@ -23,9 +23,6 @@ BUILD = os.path.join(PKG, "build")
 VARIANTS = {
     "base": {},
     "pingpong": {"FA_FWD_PINGPONG": 1},
-    "pingpong_setprio": {"FA_FWD_PINGPONG": 1, "FA_FWD_SETPRIO": 1},
-    "pingpong_1wg": {"FA_FWD_PINGPONG": 1, "FA_FWD_LDS_PAD": 96 * 1024},
-    "pingpong_mfmasum": {"FA_FWD_PINGPONG": 1, "FA_FWD_MFMA_SUM": 1},
 }
 
 CONFIGS = [
@@ -46,7 +43,7 @@ def build(names):
 
     def one(name):
         defs = VARIANTS[name]
-        extra = [f"-D{k}={v}" for k, v in defs.items()]
+        extra = [k if k.startswith("-") else f"-D{k}={v}" for k, v in defs.items()]
         objs = []
         for tu in ("fa_d32.hip", "fa_d64.hip", "fa_d128.hip"):
             obj = os.path.join(BUILD, f"var_{name}_{tu}.o")
