@@ -79,12 +79,32 @@ int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {
         case FA_QUERY_RNG_INCREMENT: return 4;
         case FA_QUERY_FWD_ARGS_SIZE: return (int64_t)sizeof(FaFwdArgs);
         case FA_QUERY_BWD_ARGS_SIZE: return (int64_t)sizeof(FaBwdArgs);
+        case FA_QUERY_MASK_ARGS_SIZE: return (int64_t)sizeof(FaBlockMask);
         default: return -1;
     }
 }
 
-int fa_fwd(const FaFwdArgs *a, void *stream) {
-    g_last_error.clear();
+}  // extern "C"
+
+namespace {
+
+// Block-sparse layout checks (fa_fwd_block / fa_bwd_block).
+int check_mask(const FaBlockMask *m, int max_q, int max_k, const char *fn) {
+    if (m == nullptr || m->mask == nullptr) return fail(FA_ERR_INVALID_ARGUMENT, "%s: blockmask is NULL", fn);
+    if (m->cols <= 0 || m->cols > 64)
+        return fail(FA_ERR_UNSUPPORTED, "%s: blockmask columns must be in [1, 64] (max_seqlen_k <= 16384)", fn);
+    if (m->row_stride < m->cols) return fail(FA_ERR_INVALID_ARGUMENT, "%s: blockmask row_stride < cols", fn);
+    if ((int64_t)m->rows * 16 < max_q || (int64_t)m->cols * 256 < max_k)
+        return fail(FA_ERR_INVALID_ARGUMENT,
+                    "%s: blockmask (%d x %d) does not cover max_seqlen_q=%d / max_seqlen_k=%d (16 x 256 blocks)", fn,
+                    m->rows, m->cols, max_q, max_k);
+    if (max_q > 32768) return fail(FA_ERR_UNSUPPORTED, "%s: block-sparse max_seqlen_q must be <= 32768", fn);
+    return FA_OK;
+}
+
+const FaBlockMask kDense = {nullptr, 0, 0, 0};
+
+int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
     int rc = check_common(a, "fa_fwd");
     if (rc) return rc;
     if (!a->o) return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: o is NULL");
@@ -103,20 +123,19 @@ int fa_fwd(const FaFwdArgs *a, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
     switch (pick_tile(a->head_dim)) {
-        case 32: e = fa::launch_fwd<32>(*a, s); break;
-        case 64: e = fa::launch_fwd<64>(*a, s); break;
-        default: e = fa::launch_fwd<128>(*a, s); break;
+        case 32: e = fa::launch_fwd<32>(*a, bm, s); break;
+        case 64: e = fa::launch_fwd<64>(*a, bm, s); break;
+        default: e = fa::launch_fwd<128>(*a, bm, s); break;
     }
     if (e != hipSuccess) return hip_fail(e, "fa_fwd launch");
     if (a->s_dmask) {
-        e = fa::launch_probs(*a, s);
+        e = fa::launch_probs(*a, bm, s);
         if (e != hipSuccess) return hip_fail(e, "fa_fwd probs launch");
     }
     return FA_OK;
 }
 
-int fa_bwd(const FaBwdArgs *a, void *stream) {
-    g_last_error.clear();
+int bwd_impl(const FaBwdArgs *a, const FaBlockMask &bm, void *stream) {
     int rc = check_common(a, "fa_bwd");
     if (rc) return rc;
     if (!a->dout || !a->out || !a->dq || !a->dk || !a->dv || !a->softmax_d || !a->dq_accum)
@@ -134,15 +153,45 @@ int fa_bwd(const FaBwdArgs *a, void *stream) {
     if (e != hipSuccess) return hip_fail(e, "fa_bwd pre launch");
     if (a->max_seqlen_k > 0) {
         switch (pick_tile(a->head_dim)) {
-            case 32: e = fa::launch_bwd<32>(*a, s); break;
-            case 64: e = fa::launch_bwd<64>(*a, s); break;
-            default: e = fa::launch_bwd<128>(*a, s); break;
+            case 32: e = fa::launch_bwd<32>(*a, bm, s); break;
+            case 64: e = fa::launch_bwd<64>(*a, bm, s); break;
+            default: e = fa::launch_bwd<128>(*a, bm, s); break;
         }
         if (e != hipSuccess) return hip_fail(e, "fa_bwd launch");
     }
     e = fa::launch_bwd_post(*a, s);
     if (e != hipSuccess) return hip_fail(e, "fa_bwd post launch");
     return FA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fa_fwd(const FaFwdArgs *a, void *stream) {
+    g_last_error.clear();
+    return fwd_impl(a, kDense, stream);
+}
+
+int fa_bwd(const FaBwdArgs *a, void *stream) {
+    g_last_error.clear();
+    return bwd_impl(a, kDense, stream);
+}
+
+int fa_fwd_block(const FaFwdArgs *a, const FaBlockMask *m, void *stream) {
+    g_last_error.clear();
+    if (a == nullptr) return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd_block: args is NULL");
+    int rc = check_mask(m, a->max_seqlen_q, a->max_seqlen_k, "fa_fwd_block");
+    if (rc) return rc;
+    return fwd_impl(a, *m, stream);
+}
+
+int fa_bwd_block(const FaBwdArgs *a, const FaBlockMask *m, void *stream) {
+    g_last_error.clear();
+    if (a == nullptr) return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd_block: args is NULL");
+    int rc = check_mask(m, a->max_seqlen_q, a->max_seqlen_k, "fa_bwd_block");
+    if (rc) return rc;
+    return bwd_impl(a, *m, stream);
 }
 
 }  // extern "C"

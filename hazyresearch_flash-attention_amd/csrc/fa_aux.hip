@@ -5,21 +5,21 @@
 namespace fa {
 
 template <typename T, bool CAUSAL, bool DROPOUT>
-static hipError_t launch_probs_t(const FaFwdArgs &a, hipStream_t stream) {
+static hipError_t launch_probs_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     dim3 grid((a.s_rows + 31) / 32, a.nheads, a.batch);
-    hipLaunchKernelGGL((fa_probs_kernel<T, CAUSAL, DROPOUT>), grid, dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((fa_probs_kernel<T, CAUSAL, DROPOUT>), grid, dim3(256), 0, stream, a, bm);
     return hipGetLastError();
 }
 
 template <typename T>
-static hipError_t launch_probs_dt(const FaFwdArgs &a, hipStream_t s) {
+static hipError_t launch_probs_dt(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t s) {
     const bool dropout = a.p_dropout > 0.f;
-    if (a.is_causal) return dropout ? launch_probs_t<T, true, true>(a, s) : launch_probs_t<T, true, false>(a, s);
-    return dropout ? launch_probs_t<T, false, true>(a, s) : launch_probs_t<T, false, false>(a, s);
+    if (a.is_causal) return dropout ? launch_probs_t<T, true, true>(a, bm, s) : launch_probs_t<T, true, false>(a, bm, s);
+    return dropout ? launch_probs_t<T, false, true>(a, bm, s) : launch_probs_t<T, false, false>(a, bm, s);
 }
 
-hipError_t launch_probs(const FaFwdArgs &a, hipStream_t s) {
-    return a.dtype == FA_DTYPE_BF16 ? launch_probs_dt<Bf16>(a, s) : launch_probs_dt<Fp16>(a, s);
+hipError_t launch_probs(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t s) {
+    return a.dtype == FA_DTYPE_BF16 ? launch_probs_dt<Bf16>(a, bm, s) : launch_probs_dt<Fp16>(a, bm, s);
 }
 
 hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t s) {

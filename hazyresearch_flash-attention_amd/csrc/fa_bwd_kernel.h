@@ -45,7 +45,9 @@ struct BwdCfg {
     static constexpr int OFF_DS = OFF_DO + 2 * Q_IMG;
     static constexpr int OFF_LSE = OFF_DS + DS_IMG;      // lse[2][BQ]
     static constexpr int OFF_DELTA = OFF_LSE + 2 * BQ * 4;
-    static constexpr int LDS_BYTES = OFF_DELTA + 2 * BQ * 4;
+    static constexpr int OFF_QLIVE = OFF_DELTA + 2 * BQ * 4;   // block-sparse: live query tiles, 1 bit each
+    static constexpr int QLIVE_WORDS = 16;                      // <= 1024 tiles (32768 rows)
+    static constexpr int LDS_BYTES = OFF_QLIVE + QLIVE_WORDS * 8;
     static constexpr int QCH = (BQ * NC + NT - 1) / NT;   // staged 16-B chunks per thread per tile
 };
 
@@ -115,8 +117,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
 #else
 #define FA_BWD_BOUNDS(C) __launch_bounds__(64 * BwdWaves<C>::value)
 #endif
-template <int D, typename T, bool CAUSAL, bool DROPOUT>
-__global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a) {
+template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false>
+__global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaBlockMask bm) {
     using C = BwdCfg<D, BwdWaves<CAUSAL>::value>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
@@ -240,20 +242,58 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a) {
             del_s[buf * C::BQ + tid] = del_st;
         }
     };
-    if (nqt > 0) {
-        gload_qtile(q_begin);
+    // ---- block sparsity (fa_bwd_block): this workgroup's keys lie in one 256-key column block
+    // cb; a 32-row query tile is live when either of its 16-row blocks is 1 in column cb. The
+    // live tiles are kept as a bit set in LDS and walked in order; dead tiles are never loaded.
+    uint64_t *qlive = (uint64_t *)(smem + C::OFF_QLIVE);
+    const int cb = k0 >> 8;
+    auto row_live = [&](int r) __attribute__((always_inline)) -> bool {
+        return r < bm.rows && bm.mask[(int64_t)r * bm.row_stride + cb] != 0;
+    };
+    if constexpr (SPARSE) {
+        for (int chunk = wave; chunk < C::QLIVE_WORDS; chunk += C::NW) {
+            const int t = 64 * chunk + lane;
+            const int rb = (q_begin >> 4) + 2 * t;
+            const bool live = t < nqt && (row_live(rb) || row_live(rb + 1));
+            const uint64_t word = __builtin_amdgcn_ballot_w64(live);
+            if (lane == 0) qlive[chunk] = word;
+        }
+        __syncthreads();
+    }
+    auto next_qt = [&](int t) __attribute__((always_inline)) -> int {
+        int n = t + 1;
+        if constexpr (!SPARSE) {
+            return n;
+        } else {
+            while (n < nqt) {
+                const int w = n >> 6;
+                const uint64_t bits = qlive[w] >> (n & 63);
+                const uint64_t ub = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bits >> 32)) << 32) |
+                                    __builtin_amdgcn_readfirstlane((uint32_t)bits);
+                if (ub) return n + (int)__builtin_ctzll(ub);
+                n = 64 * (w + 1);
+            }
+            return nqt;
+        }
+    };
+    const int t_first = SPARSE ? next_qt(-1) : 0;
+    if (t_first < nqt) {
+        gload_qtile(q_begin + t_first * C::BQ);
         lds_store_qtile(0);
     }
     __syncthreads();
 
-    auto qstep = [&](auto par_tag, int it) __attribute__((always_inline)) {
+    auto qstep = [&](auto par_tag, int it, int itn) __attribute__((always_inline)) {
         constexpr int BUF = decltype(par_tag)::value;
         char *qimg = smem + C::OFF_Q + BUF * C::Q_IMG;
         char *doimg = smem + C::OFF_DO + BUF * C::Q_IMG;
         const float *lse_b = lse_s + BUF * C::BQ;
         const float *del_b = del_s + BUF * C::BQ;
         const int q0 = q_begin + it * C::BQ;
-        if (it + 1 < nqt) gload_qtile(q0 + C::BQ);
+        if (itn < nqt) gload_qtile(q_begin + itn * C::BQ);
+        // block sparsity: a dead 16-row half of a live tile is masked (P = 0 there)
+        const bool dead0 = SPARSE && !row_live(q0 >> 4);
+        const bool dead1 = SPARSE && !row_live((q0 >> 4) + 1);
         const bool active = !CAUSAL || (q0 + C::BQ - 1 >= kw);
         if (active) {
             // ---- S = Q K^T and dZ = dO V^T : lane = key, registers = query rows crow(r,hi)
@@ -269,7 +309,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a) {
             }
             // row constants for rows crow(4g+e, hi) = 8g + 4hi + e (16-B aligned groups of 4)
             const bool need_mask = (q0 + C::BQ > seqlen_q) || (k0 + C::BKV > seqlen_k) ||
-                                   (CAUSAL && q0 < kw + 31);
+                                   (CAUSAL && q0 < kw + 31) || dead0 || dead1;
             u32x4 rw[2];
             if (DROPOUT) {
 #pragma unroll
@@ -290,7 +330,8 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a) {
                     float p = fast_exp2(fmaf(sacc[r], c_log2, -lse4[e]));
                     if (need_mask) {
                         const int q = q0 + crow(r, hi);
-                        if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
+                        if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q) || (r < 8 ? dead0 : dead1))
+                            p = 0.f;
                     }
                     float dpv = zacc[r];
                     float pdv = p;
@@ -376,12 +417,25 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a) {
                 }
             }
         }
-        if (it + 1 < nqt) lds_store_qtile(1 - BUF);
+        if (itn < nqt) lds_store_qtile(1 - BUF);
         __syncthreads();
     };
-    for (int it = 0; it < nqt; it += 2) {
-        qstep(std::integral_constant<int, 0>(), it);
-        if (it + 1 < nqt) qstep(std::integral_constant<int, 1>(), it + 1);
+    if constexpr (SPARSE) {
+        int it = t_first;
+        while (it < nqt) {
+            int itn = next_qt(it);
+            qstep(std::integral_constant<int, 0>(), it, itn);
+            it = itn;
+            if (it >= nqt) break;
+            itn = next_qt(it);
+            qstep(std::integral_constant<int, 1>(), it, itn);
+            it = itn;
+        }
+    } else {
+        for (int it = 0; it < nqt; it += 2) {
+            qstep(std::integral_constant<int, 0>(), it, it + 1);
+            if (it + 1 < nqt) qstep(std::integral_constant<int, 1>(), it + 1, it + 2);
+        }
     }
 
     // ---- epilogue: dV, dK (scaled) rows of this lane's key
@@ -411,7 +465,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a) {
 // s[b][h][row][col] = softmax(scale*QK^T)[row][col], negated where dropout dropped it,
 // 0 where masked or padded. Row-major (B, H, s_rows, s_cols).
 template <typename T, bool CAUSAL, bool DROPOUT>
-__global__ __launch_bounds__(256) void fa_probs_kernel(const FaFwdArgs a) {
+__global__ __launch_bounds__(256) void fa_probs_kernel(const FaFwdArgs a, const FaBlockMask bm) {
     // block = 32 query rows x 64 keys; thread = one key column x 8 rows (one Philox call)
     constexpr float LOG2E = 1.4426950408889634f;
     __shared__ float qs[32][129];
@@ -461,7 +515,8 @@ __global__ __launch_bounds__(256) void fa_probs_kernel(const FaFwdArgs a) {
             const int q = q0 + r;
             if (q >= a.s_rows) continue;
             float val = 0.f;
-            const bool valid = q < seqlen_q && col < seqlen_k && !(CAUSAL && col > q);
+            bool valid = q < seqlen_q && col < seqlen_k && !(CAUSAL && col > q);
+            if (valid && bm.mask) valid = (q >> 4) < bm.rows && bm.mask[(int64_t)(q >> 4) * bm.row_stride + (col >> 8)] != 0;
             if (valid) {
                 float acc = 0.f;
                 for (int d = 0; d < D; ++d) acc = fmaf(qs[r][d], ks[col_l][d], acc);

@@ -119,8 +119,8 @@ __device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
 #define FA_FWD_BOUNDS(NW) __launch_bounds__(64 * NW)
 #endif
 
-template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW>
-__global__ FA_FWD_BOUNDS(NW) void fa_fwd_kernel(const FaFwdArgs a) {
+template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
+__global__ FA_FWD_BOUNDS(NW) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
     using C = FwdCfg<D, NW>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
@@ -171,6 +171,47 @@ __global__ FA_FWD_BOUNDS(NW) void fa_fwd_kernel(const FaFwdArgs a) {
     int n_end = seqlen_k;
     if (CAUSAL) n_end = min(n_end, q0 + C::BM);
     const int nt = (n_end + C::BN - 1) / C::BN;
+
+    // ---- block sparsity (fa_fwd_block): this lane's live 256-key column blocks, and their union
+    // over the workgroup's rows, which drives the tile walk (dead columns are never loaded)
+    uint64_t lane_cols = ~0ull, wg_cols = ~0ull;
+    if constexpr (SPARSE) {
+        lane_cols = 0;
+        const int rb = qrow >> 4;
+        if (qrow < seqlen_q && rb < bm.rows) {
+            const uint8_t *mr = bm.mask + (int64_t)rb * bm.row_stride;
+            for (int c = 0; c < bm.cols; ++c)
+                if (mr[c]) lane_cols |= 1ull << c;
+        }
+        uint32_t lo = (uint32_t)lane_cols, hv = (uint32_t)(lane_cols >> 32);
+#pragma unroll
+        for (int sh = 1; sh < 64; sh <<= 1) {
+            lo |= (uint32_t)__shfl_xor((int)lo, sh);
+            hv |= (uint32_t)__shfl_xor((int)hv, sh);
+        }
+        uint64_t *wcols = (uint64_t *)smem;
+        if (lane == 0) wcols[wave] = ((uint64_t)hv << 32) | lo;
+        __syncthreads();
+        wg_cols = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) wg_cols |= wcols[w];
+        wg_cols = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wg_cols >> 32)) << 32) |
+                  __builtin_amdgcn_readfirstlane((uint32_t)wg_cols);
+        __syncthreads();   // the K image reuses these bytes
+    }
+    // next live 64-key tile after j (dense: j + 1; sparse: skip dead 256-key column blocks)
+    auto next_tile = [&](int j) __attribute__((always_inline)) -> int {
+        const int n = j + 1;
+        if constexpr (!SPARSE) {
+            return n;
+        } else {
+            const int c = n >> 2;
+            if (c >= 64) return nt;
+            if ((wg_cols >> c) & 1) return n;
+            const uint64_t rest = c + 1 < 64 ? (wg_cols >> (c + 1)) : 0ull;
+            return rest ? 4 * (c + 1 + (int)__builtin_ctzll(rest)) : nt;
+        }
+    };
 
     // ---- Q fragments (B operand of S^T = K Q^T): Q[qrow][16ks + 8hi + j]
     typename T::frag qf[D / 16];
@@ -280,14 +321,16 @@ __global__ FA_FWD_BOUNDS(NW) void fa_fwd_kernel(const FaFwdArgs a) {
     // ---- softmax of one tile in registers: mask, max, deferred rescale, exp, row sum,
     // dropout, and conversion into the 16-bit B operand of P·V.
     auto softmax_tile = [&](f32x16 (&s)[2], int kv0, typename T::frag (&pf)[2][2]) __attribute__((always_inline)) {
-        const bool need_mask = (kv0 + C::BN > seqlen_k) || (CAUSAL && kv0 + C::BN - 1 > qw);
+        const bool dead = SPARSE && !((lane_cols >> (kv0 >> 8)) & 1);   // row's block is 0 in the layout
+        const bool need_mask = (kv0 + C::BN > seqlen_k) || (CAUSAL && kv0 + C::BN - 1 > qw) ||
+                               (SPARSE && __builtin_amdgcn_ballot_w64(dead));
         if (need_mask) {
 #pragma unroll
             for (int st = 0; st < 2; ++st)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int kv = kv0 + 32 * st + crow(r, hi);
-                    if (kv >= seqlen_k || (CAUSAL && kv > qrow)) s[st][r] = -INFINITY;
+                    if (dead || kv >= seqlen_k || (CAUSAL && kv > qrow)) s[st][r] = -INFINITY;
                 }
         }
         const float mx = pair_max(max_tree32(s[0], s[1]));
@@ -459,20 +502,55 @@ __global__ FA_FWD_BOUNDS(NW) void fa_fwd_kernel(const FaFwdArgs a) {
         __syncthreads();
     };
 
-    // prologue: K[0] -> kbuf0, V[0] -> vbuf0 (+ K[1] -> kbuf1 and S of tile 0 when pipelined)
-    gload_k(0);
-    gload_v(0);
-    lds_store_k(smem);
-    lds_store_v(smem + 2 * C::TILE_BYTES);
-    if (FA_FWD_PIPE) {
-        gload_k(1);
-        lds_store_k(smem + C::TILE_BYTES);
-    }
-    __syncthreads();
-    if (FA_FWD_PIPE) qk(smem, sA);
-    for (int j = 0; j < nt; j += 2) {
-        step(std::integral_constant<int, 0>(), j);
-        if (j + 1 < nt) step(std::integral_constant<int, 1>(), j + 1);
+    if constexpr (SPARSE) {
+        // walk the live tiles only: the same double-buffered step with tile indices from
+        // next_tile (a dead next tile is never loaded)
+        auto sstep = [&](auto par_tag, int j, int jn) __attribute__((always_inline)) {
+            constexpr int P = decltype(par_tag)::value;
+            char *kb_rd = smem + P * C::TILE_BYTES;
+            char *vb_rd = smem + (2 + P) * C::TILE_BYTES;
+            gload_k(jn);
+            gload_v(jn);
+            f32x16 s[2];
+            qk(kb_rd, s);
+            typename T::frag pf[2][2];
+            softmax_tile(s, j * C::BN, pf);
+            pv(vb_rd, pf);
+            lds_store_k(smem + (1 - P) * C::TILE_BYTES);
+            lds_store_v(smem + (3 - P) * C::TILE_BYTES);
+            __syncthreads();
+        };
+        int j = next_tile(-1);
+        gload_k(j);
+        gload_v(j);
+        lds_store_k(smem);
+        lds_store_v(smem + 2 * C::TILE_BYTES);
+        __syncthreads();
+        while (j < nt) {
+            int jn = next_tile(j);
+            sstep(std::integral_constant<int, 0>(), j, jn);
+            j = jn;
+            if (j >= nt) break;
+            jn = next_tile(j);
+            sstep(std::integral_constant<int, 1>(), j, jn);
+            j = jn;
+        }
+    } else {
+        // prologue: K[0] -> kbuf0, V[0] -> vbuf0 (+ K[1] -> kbuf1 and S of tile 0 when pipelined)
+        gload_k(0);
+        gload_v(0);
+        lds_store_k(smem);
+        lds_store_v(smem + 2 * C::TILE_BYTES);
+        if (FA_FWD_PIPE) {
+            gload_k(1);
+            lds_store_k(smem + C::TILE_BYTES);
+        }
+        __syncthreads();
+        if (FA_FWD_PIPE) qk(smem, sA);
+        for (int j = 0; j < nt; j += 2) {
+            step(std::integral_constant<int, 0>(), j);
+            if (j + 1 < nt) step(std::integral_constant<int, 1>(), j + 1);
+        }
     }
 #endif
 

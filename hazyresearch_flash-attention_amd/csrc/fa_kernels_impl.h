@@ -8,16 +8,16 @@
 
 namespace fa {
 
-template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW>
-static hipError_t launch_fwd_nw(const FaFwdArgs &a, hipStream_t stream) {
+template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
+static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     using C = FwdCfg<D, NW>;
     const int lds = C::lds_bytes(DROPOUT);
-    auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT, NW>;
+    auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT, NW, SPARSE>;
     static const hipError_t attr_err =
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (attr_err != hipSuccess) return attr_err;
     dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a);
+    hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a, bm);
     return hipGetLastError();
 }
 
@@ -33,48 +33,55 @@ static int pick_fwd_waves(const FaFwdArgs &) {
 }
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
-static hipError_t launch_fwd_t(const FaFwdArgs &a, hipStream_t stream) {
+static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
+    if (bm.mask) return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8, true>(a, bm, stream);
     switch (pick_fwd_waves(a)) {
-        case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, stream);
-        case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, stream);
-        default: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 2>(a, stream);
+        case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
+        case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, bm, stream);
+        default: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 2>(a, bm, stream);
     }
 }
 
-template <int D, typename T, bool CAUSAL, bool DROPOUT>
-static hipError_t launch_bwd_t(const FaBwdArgs &a, hipStream_t stream) {
+template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE>
+static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     using C = BwdCfg<D, BwdWaves<CAUSAL>::value>;
-    auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT>;
+    auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT, SPARSE>;
     static const hipError_t attr_err =
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
     if (attr_err != hipSuccess) return attr_err;
     dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a);
+    hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
     return hipGetLastError();
 }
 
-template <int D, typename T>
-static hipError_t launch_fwd_dt(const FaFwdArgs &a, hipStream_t s) {
-    const bool dropout = a.p_dropout > 0.f;
-    if (a.is_causal) return dropout ? launch_fwd_t<D, T, true, true>(a, s) : launch_fwd_t<D, T, true, false>(a, s);
-    return dropout ? launch_fwd_t<D, T, false, true>(a, s) : launch_fwd_t<D, T, false, false>(a, s);
+template <int D, typename T, bool CAUSAL, bool DROPOUT>
+static hipError_t launch_bwd_t(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
+    return bm.mask ? launch_bwd_s<D, T, CAUSAL, DROPOUT, true>(a, bm, stream)
+                   : launch_bwd_s<D, T, CAUSAL, DROPOUT, false>(a, bm, stream);
 }
 
 template <int D, typename T>
-static hipError_t launch_bwd_dt(const FaBwdArgs &a, hipStream_t s) {
+static hipError_t launch_fwd_dt(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t s) {
     const bool dropout = a.p_dropout > 0.f;
-    if (a.is_causal) return dropout ? launch_bwd_t<D, T, true, true>(a, s) : launch_bwd_t<D, T, true, false>(a, s);
-    return dropout ? launch_bwd_t<D, T, false, true>(a, s) : launch_bwd_t<D, T, false, false>(a, s);
+    if (a.is_causal) return dropout ? launch_fwd_t<D, T, true, true>(a, bm, s) : launch_fwd_t<D, T, true, false>(a, bm, s);
+    return dropout ? launch_fwd_t<D, T, false, true>(a, bm, s) : launch_fwd_t<D, T, false, false>(a, bm, s);
+}
+
+template <int D, typename T>
+static hipError_t launch_bwd_dt(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t s) {
+    const bool dropout = a.p_dropout > 0.f;
+    if (a.is_causal) return dropout ? launch_bwd_t<D, T, true, true>(a, bm, s) : launch_bwd_t<D, T, true, false>(a, bm, s);
+    return dropout ? launch_bwd_t<D, T, false, true>(a, bm, s) : launch_bwd_t<D, T, false, false>(a, bm, s);
 }
 
 }  // namespace fa
 
 #define FA_INSTANTIATE(D)                                                                        \
     namespace fa {                                                                               \
-    template <> hipError_t launch_fwd<D>(const FaFwdArgs &a, hipStream_t s) {                    \
-        return a.dtype == FA_DTYPE_BF16 ? launch_fwd_dt<D, Bf16>(a, s) : launch_fwd_dt<D, Fp16>(a, s); \
+    template <> hipError_t launch_fwd<D>(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t s) { \
+        return a.dtype == FA_DTYPE_BF16 ? launch_fwd_dt<D, Bf16>(a, bm, s) : launch_fwd_dt<D, Fp16>(a, bm, s); \
     }                                                                                            \
-    template <> hipError_t launch_bwd<D>(const FaBwdArgs &a, hipStream_t s) {                    \
-        return a.dtype == FA_DTYPE_BF16 ? launch_bwd_dt<D, Bf16>(a, s) : launch_bwd_dt<D, Fp16>(a, s); \
+    template <> hipError_t launch_bwd<D>(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t s) { \
+        return a.dtype == FA_DTYPE_BF16 ? launch_bwd_dt<D, Bf16>(a, bm, s) : launch_bwd_dt<D, Fp16>(a, bm, s); \
     }                                                                                            \
     }

@@ -5,9 +5,10 @@
 
 namespace fa {
 // D is the padded head-dim tile (32, 64 or 128); the kernels zero-fill head_dim < D.
-template <int D> hipError_t launch_fwd(const FaFwdArgs &a, hipStream_t stream);
-template <int D> hipError_t launch_bwd(const FaBwdArgs &a, hipStream_t stream);
-hipError_t launch_probs(const FaFwdArgs &a, hipStream_t stream);
+// bm.mask == nullptr: dense; otherwise the block-sparse kernels (fa_fwd_block / fa_bwd_block).
+template <int D> hipError_t launch_fwd(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
+template <int D> hipError_t launch_bwd(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
+hipError_t launch_probs(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
 hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t stream);
 hipError_t launch_bwd_post(const FaBwdArgs &a, hipStream_t stream);
 }  // namespace fa

@@ -26,6 +26,7 @@ FA_QUERY_MAX_HEAD_DIM = 2
 FA_QUERY_RNG_INCREMENT = 3
 FA_QUERY_FWD_ARGS_SIZE = 4
 FA_QUERY_BWD_ARGS_SIZE = 5
+FA_QUERY_MASK_ARGS_SIZE = 6
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -75,6 +76,11 @@ class FaBwdArgs(ctypes.Structure):
     ]
 
 
+class FaBlockMask(ctypes.Structure):
+    """ctypes mirror of FaBlockMask (include/fa_hip.h): 0/1 bytes, 16-query x 256-key blocks."""
+    _fields_ = [("mask", _vp), ("row_stride", _i64), ("rows", _i32), ("cols", _i32)]
+
+
 _lib_handle = None
 
 
@@ -91,6 +97,10 @@ def lib():
         h.fa_fwd.restype = ctypes.c_int
         h.fa_bwd.argtypes = [ctypes.POINTER(FaBwdArgs), _vp]
         h.fa_bwd.restype = ctypes.c_int
+        h.fa_fwd_block.argtypes = [ctypes.POINTER(FaFwdArgs), ctypes.POINTER(FaBlockMask), _vp]
+        h.fa_fwd_block.restype = ctypes.c_int
+        h.fa_bwd_block.argtypes = [ctypes.POINTER(FaBwdArgs), ctypes.POINTER(FaBlockMask), _vp]
+        h.fa_bwd_block.restype = ctypes.c_int
         h.fa_query.argtypes = [ctypes.c_int, _i64, _i64, _i64]
         h.fa_query.restype = _i64
         h.fa_last_error.argtypes = []
@@ -101,6 +111,8 @@ def lib():
             raise ImportError("FaFwdArgs layout mismatch between fa_hip.h and flash_attn_hip.py")
         if h.fa_query(FA_QUERY_BWD_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaBwdArgs):
             raise ImportError("FaBwdArgs layout mismatch between fa_hip.h and flash_attn_hip.py")
+        if h.fa_query(FA_QUERY_MASK_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaBlockMask):
+            raise ImportError("FaBlockMask layout mismatch between fa_hip.h and flash_attn_hip.py")
         _lib_handle = h
     return _lib_handle
 
@@ -165,9 +177,21 @@ def _raise(rc, what):
     raise RuntimeError(f"{what} failed (code {rc}): {msg}")
 
 
+def _mask_struct(layout, dev):
+    """FaBlockMask for a 0/1 layout tensor (rows = 16-query blocks, cols = 256-key blocks)."""
+    _check(layout.dim() == 2, "blockmask layout must be 2-D (seqlen/16, seqlen/256)")
+    _check(layout.device == dev, "blockmask must be on the device of q")
+    if layout.dtype != torch.uint8 or layout.stride(-1) != 1:
+        layout = layout.to(torch.uint8).contiguous()
+    m = FaBlockMask()
+    m.mask, m.row_stride, m.rows, m.cols = layout.data_ptr(), layout.stride(0), layout.shape[0], layout.shape[1]
+    return m, layout
+
+
 def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropout, softmax_scale,
-        zero_tensors, is_causal, return_softmax, gen, rng_state=None):
-    """Forward pass; same arguments and result as the reference's `flash_attn_cuda.fwd`."""
+        zero_tensors, is_causal, return_softmax, gen, rng_state=None, layout=None):
+    """Forward pass; same arguments and result as the reference's `flash_attn_cuda.fwd`.
+    `layout` (optional, 0/1 (seqlen/16, seqlen/256) on the device) selects the block-sparse kernel."""
     dt = _dtype_code(q.dtype)
     _check(k.dtype == q.dtype and v.dtype == q.dtype, "q, k, v must have the same dtype")
     _check(cu_seqlens_q.dtype == torch.int32 and cu_seqlens_k.dtype == torch.int32, "cu_seqlens must be int32")
@@ -222,7 +246,11 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
         a.rng_seed, a.rng_offset = seed, offset
         a.is_causal = 1 if is_causal else 0
         a.dtype = dt
-        rc = lib().fa_fwd(ctypes.byref(a), _stream_ptr(dev))
+        if layout is None:
+            rc = lib().fa_fwd(ctypes.byref(a), _stream_ptr(dev))
+        else:
+            m, _keep = _mask_struct(layout, dev)
+            rc = lib().fa_fwd_block(ctypes.byref(a), ctypes.byref(m), _stream_ptr(dev))
         if rc != 0:
             _raise(rc, "fa_fwd")
     result = [o, lse]
@@ -232,7 +260,7 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
 
 
 def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
-        p_dropout, softmax_scale, zero_tensors, is_causal, gen, rng_state=None):
+        p_dropout, softmax_scale, zero_tensors, is_causal, gen, rng_state=None, layout=None):
     """Backward pass with the signature flash_attn_interface.py:31-33 expects. Writes dq, dk, dv
     in place (strided views allowed) and returns softmax_d = rowsum(dout * out), (B, H, lse_stride)."""
     dt = _dtype_code(q.dtype)
@@ -288,7 +316,48 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
         a.rng_seed, a.rng_offset = seed, offset
         a.is_causal = 1 if is_causal else 0
         a.dtype = dt
-        rc = lib().fa_bwd(ctypes.byref(a), _stream_ptr(dev))
+        if layout is None:
+            rc = lib().fa_bwd(ctypes.byref(a), _stream_ptr(dev))
+        else:
+            m, _keep = _mask_struct(layout, dev)
+            rc = lib().fa_bwd_block(ctypes.byref(a), ctypes.byref(m), _stream_ptr(dev))
         if rc != 0:
             _raise(rc, "fa_bwd")
     return softmax_d
+
+
+def decode_blockmask(blockmask, nrow=None):
+    """Inverse of convert_blockmask (flash_attn/flash_blocksparse_attn_interface.py:8-40): the
+    (col, row) int32 list of row indices x4 (+flags, -1 padded) back to the 0/1 (row, col) layout."""
+    ncol, nr = blockmask.shape
+    nrow = nr if nrow is None else nrow
+    bm = blockmask.to(torch.int64)
+    valid = bm >= 0
+    rows = torch.div(bm.clamp(min=0), 4, rounding_mode="floor")
+    cols = torch.arange(ncol, device=bm.device).unsqueeze(1).expand_as(bm)
+    layout = torch.zeros((nrow, ncol), dtype=torch.uint8, device=bm.device)
+    layout[rows[valid], cols[valid]] = 1
+    return layout
+
+
+def fwd_block(qkv, cu_seqlens, blockmask, p_dropout, max_s, softmax_scale, is_causal, return_softmax, gen,
+              rng_state=None):
+    """`flash_attn_cuda.fwd_block` as called at flash_blocksparse_attn_interface.py:46-48: packed
+    qkv (total, 3, H, D) and the CONVERTED blockmask (convert_blockmask's int32 (col, row) list).
+    Returns [context, softmax_lse, (S_dmask)]."""
+    _check(qkv.dim() == 4 and qkv.shape[1] == 3, "qkv must be (total, 3, nheads, headdim)")
+    layout = decode_blockmask(blockmask)
+    return fwd(qkv[:, 0], qkv[:, 1], qkv[:, 2], cu_seqlens, cu_seqlens, max_s, max_s, p_dropout, softmax_scale,
+               False, is_causal, return_softmax, gen, rng_state=rng_state, layout=layout)
+
+
+def bwd_block(dout, qkv, out, S_dmask, softmax_lse, cu_seqlens, blockmask, p_dropout, softmax_scale, max_s,
+              is_causal, gen, rng_state=None):
+    """`flash_attn_cuda.bwd_block` as called at flash_blocksparse_attn_interface.py:55-58.
+    Returns (dqkv, None, softmax_d); S_dmask is not needed (the mask is replayed from Philox)."""
+    layout = decode_blockmask(blockmask)
+    dqkv = torch.empty_like(qkv)
+    softmax_d = bwd(dout, qkv[:, 0], qkv[:, 1], qkv[:, 2], out, softmax_lse, dqkv[:, 0], dqkv[:, 1], dqkv[:, 2],
+                    cu_seqlens, cu_seqlens, max_s, max_s, p_dropout, softmax_scale, False, is_causal, gen,
+                    rng_state=rng_state, layout=layout)
+    return dqkv, None, softmax_d

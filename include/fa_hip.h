@@ -8,6 +8,10 @@
  *                                                  bound at fmha_api.cpp:244-247)
  *   fa_bwd  <- flash_attn_cuda.bwd              (called at flash_attn/flash_attn_interface.py:31-33;
  *                                                  never bound in the reference, built fresh here)
+ *   fa_fwd_block <- flash_attn_cuda.fwd_block (called at flash_attn/flash_blocksparse_attn_interface.py:46-48;
+ *   fa_bwd_block <- flash_attn_cuda.bwd_block  flash_attn/flash_blocksparse_attn_interface.py:55-58;
+ *                                               declared by the reference's Python but never bound
+ *                                               natively, built fresh here)
  *   fa_query, fa_last_error, fa_version: host helpers (no reference counterpart; the reference
  *                                                  raised through TORCH_CHECK / exit(1),
  *                                                  fmha_api.cpp:131-170, fmha_utils.h:36-48)
@@ -109,6 +113,18 @@ typedef struct FaBwdArgs {
     int32_t dtype;
 } FaBwdArgs;
 
+/* Block-sparsity layout for fa_fwd_block / fa_bwd_block: the 0/1 "blockmask" of the
+ * reference (flash_attn/flash_blocksparse_attn_interface.py:8-40 before convert_blockmask;
+ * semantics of tests/test_flash_attn.py:189-215): mask[r][c] != 0 lets query rows
+ * 16r..16r+15 attend keys 256c..256c+255 (positions within each sequence). Rows with no live
+ * block produce output 0 and lse -inf. */
+typedef struct FaBlockMask {
+    const uint8_t *mask;      /* (rows, cols) bytes on the device */
+    int64_t row_stride;       /* elements between consecutive rows (>= cols) */
+    int32_t rows;             /* >= ceil(max_seqlen_q / 16) */
+    int32_t cols;             /* >= ceil(max_seqlen_k / 256), <= 64 */
+} FaBlockMask;
+
 /* Forward pass. Writes o, softmax_lse and (if s_dmask != NULL) the attention probabilities
  * softmax(QK^T*scale) in row-major (B, H, s_rows, s_cols), with dropped entries negated
  * (the sign convention of the reference, softmax.h:256-296). */
@@ -117,12 +133,20 @@ int fa_fwd(const FaFwdArgs *args, void *stream);
 /* Backward pass. Writes dq, dk, dv and softmax_d. */
 int fa_bwd(const FaBwdArgs *args, void *stream);
 
+/* Block-sparse forward / backward: as fa_fwd / fa_bwd with the layout `mask` applied on top of
+ * the key-length and causal masks. Blocks that are 0 for every row of a workgroup are skipped
+ * (no loads, no MFMAs). Limits: mask->cols <= 64 (max_seqlen_k <= 16384),
+ * max_seqlen_q <= 32768. */
+int fa_fwd_block(const FaFwdArgs *args, const FaBlockMask *mask, void *stream);
+int fa_bwd_block(const FaBwdArgs *args, const FaBlockMask *mask, void *stream);
+
 enum {
     FA_QUERY_BWD_WORKSPACE = 1,   /* a = total_q, b = nheads, c = head_dim -> bytes */
     FA_QUERY_MAX_HEAD_DIM = 2,    /* -> 128 */
     FA_QUERY_RNG_INCREMENT = 3,   /* Philox offset increment a forward reserves per call */
     FA_QUERY_FWD_ARGS_SIZE = 4,   /* sizeof(FaFwdArgs): lets FFI bindings check their struct layout */
     FA_QUERY_BWD_ARGS_SIZE = 5,   /* sizeof(FaBwdArgs) */
+    FA_QUERY_MASK_ARGS_SIZE = 6,  /* sizeof(FaBlockMask) */
 };
 int64_t fa_query(int what, int64_t a, int64_t b, int64_t c);
 

@@ -8,6 +8,8 @@ Follows /root/reference/tests/test_flash_attn.py:
   attention_ref                 :115-159 (fp32 upcast oracle; upcast=False + reorder_ops is the
                                           "PyTorch baseline error" estimator of the 2x rule :407-409)
   get_dropout_fraction          :300-329
+  attention_blocksparse_ref     :189-215 (plus causal / upcast / reorder_ops, and fully masked rows
+                                          give 0 instead of NaN, as the kernels do)
 The reference's attention_ref raises UnboundLocalError when dropout_mask is None (:153-155);
 here a missing mask means "keep everything".
 """
@@ -98,3 +100,37 @@ def max_err_bound(out_pt, out_ref, floor=0.0):
     """The reference's 2x rule (tests/test_flash_attn.py:407-409): allowed max |out - ref|.
     `floor` covers fp32 inputs, where the PyTorch baseline error can be exactly 0."""
     return max(2 * (out_pt.float() - out_ref.float()).abs().max().item(), floor)
+
+
+def attention_blocksparse_ref(qkv, blockmask, attn_mask=None, dropout_p=0.0, dropout_mask=None, causal=False,
+                              upcast=True, reorder_ops=False):
+    """qkv (B, S, 3, H, D); blockmask (S/16 rounded up, S/256 rounded up) 0/1, entry [r][c] lets
+    query rows 16r..16r+15 see keys 256c..256c+255; attn_mask (B, S) bool key/query padding
+    (True = valid); dropout_mask (B, H, S, S) bool (True = keep).
+    Returns (output (B, S, H, D), attention (B, H, S, S)) in qkv's dtype."""
+    dtype_og = qkv.dtype
+    q, k, v = qkv.unbind(dim=2)
+    if upcast:
+        q, k, v = q.float(), k.float(), v.float()
+    seqlen, d = qkv.shape[1], qkv.shape[-1]
+    if not reorder_ops:
+        scores = torch.einsum("bthd,bshd->bhts", q / math.sqrt(d), k)
+    else:
+        scores = torch.einsum("bthd,bshd->bhts", q, k / math.sqrt(d))
+    if attn_mask is not None:
+        scores.masked_fill_(~attn_mask[:, None, None, :], float("-inf"))
+    live = blockmask.to(torch.bool).repeat_interleave(16, dim=0).repeat_interleave(256, dim=1)[:seqlen, :seqlen]
+    live = live.to(scores.device)
+    scores.masked_fill_(~live[None, None], float("-inf"))
+    if causal:
+        cm = torch.triu(torch.ones(seqlen, seqlen, dtype=torch.bool, device=scores.device), 1)
+        scores.masked_fill_(cm, float("-inf"))
+    attention = torch.softmax(scores, dim=-1).nan_to_num(0.0)   # rows with no live key -> 0
+    if attn_mask is not None:
+        attention = attention.masked_fill(~attn_mask[:, None, :, None], 0.0)
+    attention = attention.masked_fill(~live[None, None], 0.0)
+    attention_drop = attention if dropout_mask is None else attention.masked_fill(~dropout_mask, 0.0)
+    output = torch.einsum("bhts,bshd->bthd", attention_drop / (1 - dropout_p), v)
+    if attn_mask is not None:
+        output.masked_fill_(~attn_mask[:, :, None, None], 0.0)
+    return output.to(dtype=dtype_og), attention.to(dtype=dtype_og)

@@ -19,7 +19,8 @@ def _declared_functions():
 
 
 def test_header_declares_the_entry_points():
-    assert _declared_functions() == ["fa_bwd", "fa_fwd", "fa_last_error", "fa_query", "fa_version"]
+    assert _declared_functions() == ["fa_bwd", "fa_bwd_block", "fa_fwd", "fa_fwd_block", "fa_last_error", "fa_query",
+                                     "fa_version"]
 
 
 def test_library_exports_every_declared_symbol():
@@ -34,6 +35,7 @@ def test_struct_layouts_match():
     L = hip.lib()
     assert L.fa_query(hip.FA_QUERY_FWD_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaFwdArgs)
     assert L.fa_query(hip.FA_QUERY_BWD_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaBwdArgs)
+    assert L.fa_query(hip.FA_QUERY_MASK_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaBlockMask)
     assert L.fa_query(hip.FA_QUERY_MAX_HEAD_DIM, 0, 0, 0) == 128
     assert L.fa_query(hip.FA_QUERY_BWD_WORKSPACE, 10, 2, 64) == 10 * 2 * 64 * 4
     assert L.fa_query(999, 0, 0, 0) == -1
@@ -68,6 +70,37 @@ def test_fwd_argument_validation(field, value, code):
     rc = L.fa_fwd(ctypes.byref(a), None)
     assert rc == code
     assert len(L.fa_last_error()) > 0
+
+
+@pytest.mark.parametrize("rows,cols,stride,code", [
+    (0, 0, 0, 1),          # NULL mask pointer (set below only when rows > 0)
+    (16, 65, 65, 2),       # more than 64 column blocks
+    (16, 1, 1, 1),         # 256 rows < max_seqlen_q = 300
+    (19, 2, 1, 1),         # row_stride < cols
+])
+def test_block_mask_validation(rows, cols, stride, code):
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    a = _valid_fwd_args(hip)
+    a.max_seqlen_q = a.max_seqlen_k = 300
+    m = hip.FaBlockMask()
+    m.mask = 4096 if rows else None
+    m.rows, m.cols, m.row_stride = rows, cols, stride
+    assert L.fa_fwd_block(ctypes.byref(a), ctypes.byref(m), None) == code
+    assert len(L.fa_last_error()) > 0
+    b = hip.FaBwdArgs()
+    b.max_seqlen_q = b.max_seqlen_k = 300
+    assert L.fa_bwd_block(ctypes.byref(b), ctypes.byref(m), None) == code
+
+
+def test_blocksparse_interface_mirrors_reference():
+    from flash_attn import flash_blocksparse_attn_interface as bsi
+    sig = lambda f: list(inspect.signature(f).parameters)
+    assert sig(bsi.flash_blocksparse_attn_func) == ["qkv", "cu_seqlens", "blockmask", "dropout_p", "max_s",
+                                                    "softmax_scale", "causal", "return_attn_probs", "convert_mask"]
+    assert sig(bsi.convert_blockmask) == ["blockmask", "causal"]
+    for cls in ("FlashBlocksparseAttnFun", "FlashBlocksparseAttnFunWithS"):
+        assert hasattr(bsi, cls)
 
 
 def test_null_args_pointer():
