@@ -185,6 +185,40 @@ def main():
         fwd_case("c4_B16_H12_S4096_D128_bf16_causal_fwd", 16, 12, 4096, 4096, 128, torch.bfloat16, True)
         fwd_case("c5_B4_H16_Sq1024_Sk4096_D64_bf16_kvpacked_fwd", 4, 16, 1024, 4096, 64, torch.bfloat16, False,
                  kvpacked=True)
+        # block-sparse forward: sliding window of +-1 256-key block plus a
+        # global first block ("local + global" layout); FLOPs counted over the live blocks only
+        from flash_attn.flash_blocksparse_attn_interface import flash_blocksparse_attn_func
+        qkv_bs = torch.randn(8 * 2048, 3, 12, 64, generator=torch.Generator().manual_seed(1)).bfloat16().to(dev)
+        cu_bs = torch.arange(0, 9 * 2048, 2048, dtype=torch.int32, device=dev)
+        rblk = torch.arange(128)[:, None] // 16
+        cblk = torch.arange(8)[None, :]
+        lay = (((rblk - cblk).abs() <= 1) | (cblk == 0)).to(dev)
+        live_frac = lay.float().mean().item()
+        ms, _ = time_events(lambda: flash_blocksparse_attn_func(qkv_bs, cu_bs, lay, 0.0, 2048), 10, 3)
+        fl = fwd_flops(8, 12, 2048, 2048, 64, False) * live_frac
+        extra["blocksparse_B8_H12_S2048_D64_bf16_local_global_fwd"] = {
+            "ms": round(ms, 4), "live_fraction": round(live_frac, 4), "TFLOPS_live": round(fl / ms / 1e9, 2),
+            "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
+        del qkv_bs
+        # var-len packing: unpad (gather) and pad (zero-filling scatter) of a
+        # (8, 2048, 12, 64) bf16 batch with random padding; algorithmic bytes = rows moved
+        from flash_attn.bert_padding import index_first_axis, index_put_first_axis
+        from oracle.attention_ref import generate_random_padding_mask
+        hs = torch.randn(8 * 2048, 12, 64, generator=torch.Generator().manual_seed(3)).bfloat16().to(dev)
+        pm = generate_random_padding_mask(2048, 8, "cpu", "third", generator=torch.Generator().manual_seed(4))
+        pidx = torch.nonzero(pm.reshape(-1)).reshape(-1).to(dev)
+        row_b = 12 * 64 * 2
+        ms_g, _ = time_events(lambda: index_first_axis(hs, pidx), 20, 3)
+        packed = index_first_axis(hs, pidx)
+        ms_p, _ = time_events(lambda: index_put_first_axis(packed, pidx, 8 * 2048), 20, 3)
+        nnz = pidx.numel()
+        extra["unpad_gather_B8_S2048_H12_D64_bf16"] = {
+            "ms": round(ms_g, 4), "GBps": round(2 * nnz * row_b / ms_g / 1e6, 1),
+            "frac_hbm": round(2 * nnz * row_b / ms_g / 1e6 / PEAK_HBM_GBS, 4), "rows": nnz}
+        extra["pad_scatter_B8_S2048_H12_D64_bf16"] = {
+            "ms": round(ms_p, 4), "GBps": round((nnz + 8 * 2048) * row_b / ms_p / 1e6, 1),
+            "frac_hbm": round((nnz + 8 * 2048) * row_b / ms_p / 1e6 / PEAK_HBM_GBS, 4)}
+        del hs, packed
         # C3 forward + backward (the fwd+bwd headline of the reference README charts)
         q3, k3, v3, _, c3q, c3k = make_inputs(8, 12, 2048, 2048, 64, torch.bfloat16, dev)
         q3.requires_grad_(); k3.requires_grad_(); v3.requires_grad_()

@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdint>
 #include <cstring>
 #include <string>
 
@@ -80,6 +81,7 @@ int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {
         case FA_QUERY_FWD_ARGS_SIZE: return (int64_t)sizeof(FaFwdArgs);
         case FA_QUERY_BWD_ARGS_SIZE: return (int64_t)sizeof(FaBwdArgs);
         case FA_QUERY_MASK_ARGS_SIZE: return (int64_t)sizeof(FaBlockMask);
+        case FA_QUERY_PAD_WORKSPACE: return a * (int64_t)sizeof(int32_t);
         default: return -1;
     }
 }
@@ -192,6 +194,57 @@ int fa_bwd_block(const FaBwdArgs *a, const FaBlockMask *m, void *stream) {
     int rc = check_mask(m, a->max_seqlen_q, a->max_seqlen_k, "fa_bwd_block");
     if (rc) return rc;
     return bwd_impl(a, *m, stream);
+}
+
+// ---- var-len packing (bert_padding)
+int fa_index_first_axis(const void *src, int64_t src_rows, int64_t src_row_stride, const int64_t *indices, int64_t n,
+                        void *dst, int64_t dst_row_stride, int64_t row_bytes, void *stream) {
+    g_last_error.clear();
+    if (n < 0 || src_rows < 0 || row_bytes < 0 || row_bytes % 2 != 0)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_first_axis: negative size or odd row_bytes");
+    if (n > 0 && row_bytes > 0 && (!src || !dst || !indices))
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_first_axis: NULL pointer");
+    if (src_row_stride < row_bytes || dst_row_stride < row_bytes || src_row_stride % 2 || dst_row_stride % 2)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_first_axis: row stride smaller than the row or odd");
+    hipError_t e = fa::launch_gather_rows(src, src_rows, src_row_stride, indices, n, dst, dst_row_stride, row_bytes,
+                                          (hipStream_t)stream);
+    return e == hipSuccess ? FA_OK : hip_fail(e, "fa_index_first_axis launch");
+}
+
+int fa_index_put_first_axis(const void *src, int64_t src_row_stride, const int64_t *indices, int64_t n, void *dst,
+                            int64_t dst_rows, int64_t dst_row_stride, int64_t row_bytes, int32_t *workspace,
+                            void *stream) {
+    g_last_error.clear();
+    if (n < 0 || dst_rows < 0 || row_bytes < 0 || row_bytes % 2 != 0)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_put_first_axis: negative size or odd row_bytes");
+    if (dst_rows > 0 && row_bytes > 0 && (!dst || !workspace || (n > 0 && (!src || !indices))))
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_put_first_axis: NULL pointer");
+    if (dst_rows > INT32_MAX || n > INT32_MAX)
+        return fail(FA_ERR_UNSUPPORTED, "fa_index_put_first_axis: more than 2^31 rows");
+    if (src_row_stride < row_bytes || dst_row_stride < row_bytes || src_row_stride % 2 || dst_row_stride % 2)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_put_first_axis: row stride smaller than the row or odd");
+    hipError_t e = fa::launch_pad_rows(src, src_row_stride, indices, n, dst, dst_rows, dst_row_stride, row_bytes,
+                                       workspace, (hipStream_t)stream);
+    return e == hipSuccess ? FA_OK : hip_fail(e, "fa_index_put_first_axis launch");
+}
+
+int fa_index_add_first_axis(const void *src, int64_t src_row_stride, const int64_t *indices, int64_t n, void *dst,
+                            int64_t dst_rows, int64_t dst_row_stride, int64_t row_elems, int32_t dtype,
+                            void *stream) {
+    g_last_error.clear();
+    if (dtype != FA_DTYPE_FP16 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_FP32)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_add_first_axis: dtype must be fp16, bf16 or fp32");
+    const int64_t esz = dtype == FA_DTYPE_FP32 ? 4 : 2;
+    if (n < 0 || dst_rows < 0 || row_elems < 0)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_add_first_axis: negative size");
+    if (n > 0 && row_elems > 0 && (!src || !dst || !indices))
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_add_first_axis: NULL pointer");
+    if (src_row_stride < row_elems * esz || dst_row_stride < row_elems * esz || src_row_stride % esz ||
+        dst_row_stride % esz)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_index_add_first_axis: bad row stride");
+    hipError_t e = fa::launch_scatter_add_rows(src, src_row_stride, indices, n, dst, dst_rows, dst_row_stride,
+                                               row_elems, dtype, (hipStream_t)stream);
+    return e == hipSuccess ? FA_OK : hip_fail(e, "fa_index_add_first_axis launch");
 }
 
 }  // extern "C"

@@ -48,6 +48,9 @@ namespace fa {
 #ifndef FA_FWD_PINGPONG
 #define FA_FWD_PINGPONG 0  // 1: two half-workgroups half a tile apart (matrix/VALU phases paired)
 #endif
+#ifndef FA_FWD_SPARSE_WPE
+#define FA_FWD_SPARSE_WPE 4   // block-sparse kernels without dropout: register budget for 4 waves/SIMD
+#endif
 #ifndef FA_FWD_LDS_PAD
 #define FA_FWD_LDS_PAD 0   // extra LDS bytes per workgroup (caps workgroups per CU; experiments)
 #endif
@@ -120,7 +123,7 @@ __device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
 #endif
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
-__global__ FA_FWD_BOUNDS(NW) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
+__global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPOUT ? FA_FWD_SPARSE_WPE : 1))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
     using C = FwdCfg<D, NW>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
@@ -511,11 +514,16 @@ __global__ FA_FWD_BOUNDS(NW) void fa_fwd_kernel(const FaFwdArgs a, const FaBlock
             char *vb_rd = smem + (2 + P) * C::TILE_BYTES;
             gload_k(jn);
             gload_v(jn);
-            f32x16 s[2];
-            qk(kb_rd, s);
-            typename T::frag pf[2][2];
-            softmax_tile(s, j * C::BN, pf);
-            pv(vb_rd, pf);
+            // a wave whose rows are all dead in this column block skips the math (it still
+            // stages its share of the next tile and meets the barrier)
+            const bool lane_live = (lane_cols >> (j >> 2)) & 1;
+            if (__builtin_amdgcn_ballot_w64(lane_live)) {
+                f32x16 s[2];
+                qk(kb_rd, s);
+                typename T::frag pf[2][2];
+                softmax_tile(s, j * C::BN, pf);
+                pv(vb_rd, pf);
+            }
             lds_store_k(smem + (1 - P) * C::TILE_BYTES);
             lds_store_v(smem + (3 - P) * C::TILE_BYTES);
             __syncthreads();

@@ -27,6 +27,7 @@ FA_QUERY_RNG_INCREMENT = 3
 FA_QUERY_FWD_ARGS_SIZE = 4
 FA_QUERY_BWD_ARGS_SIZE = 5
 FA_QUERY_MASK_ARGS_SIZE = 6
+FA_QUERY_PAD_WORKSPACE = 7
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -101,6 +102,12 @@ def lib():
         h.fa_fwd_block.restype = ctypes.c_int
         h.fa_bwd_block.argtypes = [ctypes.POINTER(FaBwdArgs), ctypes.POINTER(FaBlockMask), _vp]
         h.fa_bwd_block.restype = ctypes.c_int
+        h.fa_index_first_axis.argtypes = [_vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _vp]
+        h.fa_index_first_axis.restype = ctypes.c_int
+        h.fa_index_put_first_axis.argtypes = [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]
+        h.fa_index_put_first_axis.restype = ctypes.c_int
+        h.fa_index_add_first_axis.argtypes = [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp]
+        h.fa_index_add_first_axis.restype = ctypes.c_int
         h.fa_query.argtypes = [ctypes.c_int, _i64, _i64, _i64]
         h.fa_query.restype = _i64
         h.fa_last_error.argtypes = []

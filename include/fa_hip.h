@@ -12,6 +12,12 @@
  *   fa_bwd_block <- flash_attn_cuda.bwd_block  flash_attn/flash_blocksparse_attn_interface.py:55-58;
  *                                               declared by the reference's Python but never bound
  *                                               natively, built fresh here)
+ *   fa_index_first_axis     <- IndexFirstAxis.forward / IndexPutFirstAxis.backward
+ *                              (flash_attn/bert_padding.py:11-38, 56-61)
+ *   fa_index_put_first_axis <- IndexPutFirstAxis.forward / IndexFirstAxis.backward
+ *                              (flash_attn/bert_padding.py:41-55, 25-38); with unpad_input /
+ *                              pad_input (:99-134) on top
+ *   fa_index_add_first_axis <- IndexFirstAxisResidual.backward (flash_attn/bert_padding.py:82-94)
  *   fa_query, fa_last_error, fa_version: host helpers (no reference counterpart; the reference
  *                                                  raised through TORCH_CHECK / exit(1),
  *                                                  fmha_api.cpp:131-170, fmha_utils.h:36-48)
@@ -37,7 +43,7 @@
 extern "C" {
 #endif
 
-enum { FA_DTYPE_FP16 = 0, FA_DTYPE_BF16 = 1 };
+enum { FA_DTYPE_FP16 = 0, FA_DTYPE_BF16 = 1, FA_DTYPE_FP32 = 2 /* padding helpers only */ };
 
 /* Error codes. */
 enum {
@@ -140,6 +146,22 @@ int fa_bwd(const FaBwdArgs *args, void *stream);
 int fa_fwd_block(const FaFwdArgs *args, const FaBlockMask *mask, void *stream);
 int fa_bwd_block(const FaBwdArgs *args, const FaBlockMask *mask, void *stream);
 
+/* Var-len packing (bert_padding). Rows of `row_bytes` bytes, byte strides, int64 row indices on
+ * the device. Indices outside the valid range read as zero rows / are ignored.
+ *   fa_index_first_axis:     dst[i] = src[indices[i]]                  for i < n
+ *   fa_index_put_first_axis: dst = 0; dst[indices[i]] = src[i]         (every dst row written once;
+ *                            workspace: fa_query(FA_QUERY_PAD_WORKSPACE, dst_rows) bytes)
+ *   fa_index_add_first_axis: dst[indices[i]] += src[i] elementwise in `dtype` (FA_DTYPE_*, fp32
+ *                            allowed); indices must be unique. */
+int fa_index_first_axis(const void *src, int64_t src_rows, int64_t src_row_stride, const int64_t *indices, int64_t n,
+                        void *dst, int64_t dst_row_stride, int64_t row_bytes, void *stream);
+int fa_index_put_first_axis(const void *src, int64_t src_row_stride, const int64_t *indices, int64_t n, void *dst,
+                            int64_t dst_rows, int64_t dst_row_stride, int64_t row_bytes, int32_t *workspace,
+                            void *stream);
+int fa_index_add_first_axis(const void *src, int64_t src_row_stride, const int64_t *indices, int64_t n, void *dst,
+                            int64_t dst_rows, int64_t dst_row_stride, int64_t row_elems, int32_t dtype,
+                            void *stream);
+
 enum {
     FA_QUERY_BWD_WORKSPACE = 1,   /* a = total_q, b = nheads, c = head_dim -> bytes */
     FA_QUERY_MAX_HEAD_DIM = 2,    /* -> 128 */
@@ -147,6 +169,7 @@ enum {
     FA_QUERY_FWD_ARGS_SIZE = 4,   /* sizeof(FaFwdArgs): lets FFI bindings check their struct layout */
     FA_QUERY_BWD_ARGS_SIZE = 5,   /* sizeof(FaBwdArgs) */
     FA_QUERY_MASK_ARGS_SIZE = 6,  /* sizeof(FaBlockMask) */
+    FA_QUERY_PAD_WORKSPACE = 7,   /* a = dst_rows -> bytes of fa_index_put_first_axis's workspace */
 };
 int64_t fa_query(int what, int64_t a, int64_t b, int64_t c);
 

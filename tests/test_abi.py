@@ -19,7 +19,8 @@ def _declared_functions():
 
 
 def test_header_declares_the_entry_points():
-    assert _declared_functions() == ["fa_bwd", "fa_bwd_block", "fa_fwd", "fa_fwd_block", "fa_last_error", "fa_query",
+    assert _declared_functions() == ["fa_bwd", "fa_bwd_block", "fa_fwd", "fa_fwd_block", "fa_index_add_first_axis",
+                                     "fa_index_first_axis", "fa_index_put_first_axis", "fa_last_error", "fa_query",
                                      "fa_version"]
 
 
@@ -101,6 +102,34 @@ def test_blocksparse_interface_mirrors_reference():
     assert sig(bsi.convert_blockmask) == ["blockmask", "causal"]
     for cls in ("FlashBlocksparseAttnFun", "FlashBlocksparseAttnFunWithS"):
         assert hasattr(bsi, cls)
+
+
+def test_padding_entry_validation():
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    # zero-size calls succeed without touching a GPU; bad sizes/strides are rejected
+    assert L.fa_index_first_axis(None, 0, 128, None, 0, None, 128, 128, None) == 0
+    assert L.fa_index_first_axis(4096, 10, 64, 4096, 5, 4096, 128, 128, None) == 1       # src stride < row
+    assert L.fa_index_first_axis(4096, 10, 128, 4096, 5, 4096, 128, 127, None) == 1     # odd row bytes
+    assert L.fa_index_put_first_axis(None, 128, None, 0, None, 0, 128, 128, None, None) == 0
+    assert L.fa_index_put_first_axis(4096, 128, 4096, 5, 4096, 10, 128, 128, None, None) == 1   # no workspace
+    assert L.fa_index_add_first_axis(4096, 128, 4096, 5, 4096, 10, 128, 64, 3, None) == 1        # bad dtype
+    assert L.fa_query(hip.FA_QUERY_PAD_WORKSPACE, 100, 0, 0) == 400
+
+
+def test_bert_padding_host_path_matches_reference_semantics():
+    import torch
+    from flash_attn.bert_padding import index_first_axis_residual, pad_input, unpad_input
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(3, 7, 4, generator=g, requires_grad=True)
+    mask = torch.arange(7)[None, :] < torch.tensor([[7], [3], [5]])
+    xu, idx, cu, mx = unpad_input(x, mask)
+    assert cu.tolist() == [0, 7, 10, 15] and mx == 7 and xu.shape == (15, 4)
+    back = pad_input(xu, idx, 3, 7)
+    assert torch.equal(back, x.detach() * mask[..., None])
+    out, res = index_first_axis_residual(x.reshape(21, 4), idx)
+    (out.sum() + 2 * res.sum()).backward()
+    assert torch.equal(x.grad.reshape(21, 4)[idx], torch.full((15, 4), 3.0))
 
 
 def test_null_args_pointer():

@@ -1,0 +1,87 @@
+"""GPU parity of the HIP var-len packing (csrc/fa_padding.hip) against torch
+indexing, the reference's own algorithm (flash_attn/bert_padding.py:11-134): bit-exact, for
+16-, 4- and 2-byte row paths, strided sources, empty inputs, and the autograd functions."""
+import pytest
+import torch
+
+from oracle.attention_ref import generate_random_padding_mask
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bp():
+    from flash_attn import bert_padding
+    return bert_padding
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(8, 300, 12, 64), (3, 97, 3, 5), (2, 64, 7), (1, 3, 8)])
+@pytest.mark.parametrize("mode", ["random", "third", "full"])
+def test_unpad_pad_roundtrip(shape, dtype, mode):
+    bp = _bp()
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(*shape, generator=g).to(dtype).to(DEV)
+    mask = generate_random_padding_mask(shape[1], shape[0], "cpu", mode, generator=g).to(DEV)
+    xu, idx, cu, mx = bp.unpad_input(x, mask)
+    flat = x.reshape(shape[0] * shape[1], *shape[2:])
+    assert torch.equal(xu, flat.index_select(0, idx))
+    assert cu.dtype == torch.int32 and cu[-1].item() == int(mask.sum())
+    back = bp.pad_input(xu, idx, shape[0], shape[1])
+    ref = torch.zeros_like(flat)
+    ref.index_copy_(0, idx, xu)
+    assert torch.equal(back, ref.reshape(x.shape))
+
+
+def test_strided_source_rows():
+    bp = _bp()
+    base = torch.randn(500, 2, 48, device=DEV, dtype=torch.bfloat16)
+    src = base[:, 1]                      # row stride 96 elements, rows of 48
+    idx = torch.randperm(500, device=DEV)[:321]
+    assert torch.equal(bp.index_first_axis(src, idx), src[idx])
+    out = bp.index_put_first_axis(src[:321], idx, 500)
+    ref = torch.zeros(500, 48, device=DEV, dtype=torch.bfloat16)
+    ref[idx] = src[:321]
+    assert torch.equal(out, ref)
+
+
+def test_empty_and_all_padding():
+    bp = _bp()
+    x = torch.randn(4, 16, device=DEV)
+    idx = torch.zeros(0, dtype=torch.int64, device=DEV)
+    assert bp.index_first_axis(x, idx).shape == (0, 16)
+    assert torch.equal(bp.index_put_first_axis(x[:0], idx, 4), torch.zeros(4, 16, device=DEV))
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+def test_autograd_matches_torch(dtype):
+    bp = _bp()
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(6, 50, 4, 8, generator=g).to(dtype).to(DEV).requires_grad_()
+    mask = generate_random_padding_mask(50, 6, "cpu", "random", generator=g).to(DEV)
+    xu, idx, _, _ = bp.unpad_input(x, mask)
+    go = torch.randn(xu.shape, generator=g).to(dtype).to(DEV)
+    (gx,) = torch.autograd.grad(xu, (x,), go)
+    ref = torch.zeros(300, 4, 8, dtype=dtype, device=DEV)
+    ref[idx] = go
+    assert torch.equal(gx, ref.reshape(x.shape))
+    v = xu.detach().requires_grad_()
+    out = bp.pad_input(v, idx, 6, 50)
+    gp = torch.randn(out.shape, generator=g).to(dtype).to(DEV)
+    (gv,) = torch.autograd.grad(out, (v,), gp)
+    assert torch.equal(gv, gp.reshape(300, 4, 8)[idx])
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+def test_index_first_axis_residual(dtype):
+    bp = _bp()
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(200, 3, 16, generator=g).to(dtype).to(DEV).requires_grad_()
+    idx = torch.randperm(200, generator=g)[:120].to(DEV)
+    out, res = bp.index_first_axis_residual(x, idx)
+    go = torch.randn(out.shape, generator=g).to(dtype).to(DEV)
+    gr = torch.randn(res.shape, generator=g).to(dtype).to(DEV)
+    ref = gr.clone()   # the backward adds into grad_residual in place, like the reference's scatter_add_
+    ref.index_add_(0, idx, go)
+    (gx,) = torch.autograd.grad((out, res), (x,), (go, gr))
+    assert torch.equal(gx, ref)

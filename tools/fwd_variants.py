@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "pingpong": {"FA_FWD_PINGPONG": 1},
+    "sparse_wpe1": {"FA_FWD_SPARSE_WPE": 1},
 }
 
 CONFIGS = [
@@ -30,6 +30,7 @@ CONFIGS = [
     ("ns_B8_H12_S2048_D64", 8, 12, 2048, 2048, 64, False, "bf16"),
     ("c4_B16_H12_S4096_D128_causal", 16, 12, 4096, 4096, 128, True, "bf16"),
     ("c5_B4_H16_1024x4096_D64", 4, 16, 1024, 4096, 64, False, "bf16"),
+    ("bs_localglobal_B8_H12_S2048_D64", 8, 12, 2048, 2048, 64, False, "bf16"),   # fa_fwd_block
 ]
 
 
@@ -39,7 +40,7 @@ def build(names):
     fb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(fb)
     fb.build(verbose=False)
-    shared = [os.path.join(BUILD, s + ".o") for s in ("fa_api.cpp", "fa_aux.hip")]
+    shared = [os.path.join(BUILD, s + ".o") for s in fb.SOURCES if not s.startswith("fa_d")]
 
     def one(name):
         defs = VARIANTS[name]
@@ -72,6 +73,8 @@ def run(names, rounds, iters):
         L = ctypes.CDLL(os.path.join(BUILD, f"var_{n}.so"))
         L.fa_fwd.argtypes = [ctypes.POINTER(hip.FaFwdArgs), ctypes.c_void_p]
         L.fa_fwd.restype = ctypes.c_int
+        L.fa_fwd_block.argtypes = [ctypes.POINTER(hip.FaFwdArgs), ctypes.POINTER(hip.FaBlockMask), ctypes.c_void_p]
+        L.fa_fwd_block.restype = ctypes.c_int
         libs[n] = L
     results = {}
     for (cname, B, H, Sq, Sk, D, causal, dt) in CONFIGS:
@@ -82,7 +85,15 @@ def run(names, rounds, iters):
         v = torch.randn(B * Sk, H, D, generator=g).to(dtype).cuda()
         cq = torch.arange(0, (B + 1) * Sq, Sq, dtype=torch.int32, device="cuda")
         ck = torch.arange(0, (B + 1) * Sk, Sk, dtype=torch.int32, device="cuda")
-        ref, _lse = hip.fwd(q, k, v, cq, ck, Sq, Sk, 0.0, D ** -0.5, False, causal, False, None)
+        sparse = cname.startswith("bs_")
+        lay, m, live = None, None, 1.0
+        if sparse:   # sliding window of +-1 256-key block plus a global first block
+            rblk = torch.arange((Sq + 15) // 16)[:, None] // 16
+            cblk = torch.arange((Sk + 255) // 256)[None, :]
+            lay = (((rblk - cblk).abs() <= 1) | (cblk == 0)).to(torch.uint8).cuda()
+            live = lay.float().mean().item()
+            m, _keep = hip._mask_struct(lay, q.device)
+        ref, _lse = hip.fwd(q, k, v, cq, ck, Sq, Sk, 0.0, D ** -0.5, False, causal, False, None, layout=lay)
         outs = {}
         a = hip.FaFwdArgs()
         lse = torch.empty(B, H, (Sq + 15) // 16 * 16, dtype=torch.float32, device="cuda")
@@ -103,18 +114,20 @@ def run(names, rounds, iters):
             o = torch.empty_like(q)
             outs[n] = o
         times = {n: [] for n in names}
-        flops = 4.0 * B * H * Sq * Sk * D / (2 if causal else 1)
+        flops = 4.0 * B * H * Sq * Sk * D / (2 if causal else 1) * live
+        call = ((lambda L: L.fa_fwd_block(ctypes.byref(a), ctypes.byref(m), stream)) if sparse
+                else (lambda L: L.fa_fwd(ctypes.byref(a), stream)))
         for r in range(rounds):
             for n in names:
                 a.o = outs[n].data_ptr()
                 L = libs[n]
                 for _ in range(3):
-                    L.fa_fwd(ctypes.byref(a), stream)
+                    call(L)
                 s = torch.cuda.Event(enable_timing=True)
                 e = torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(iters):
-                    rc = L.fa_fwd(ctypes.byref(a), stream)
+                    rc = call(L)
                 e.record()
                 torch.cuda.synchronize()
                 assert rc == 0
