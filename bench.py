@@ -219,6 +219,16 @@ def main():
             "ms": round(ms_p, 4), "GBps": round((nnz + 8 * 2048) * row_b / ms_p / 1e6, 1),
             "frac_hbm": round((nnz + 8 * 2048) * row_b / ms_p / 1e6 / PEAK_HBM_GBS, 4)}
         del hs, packed
+        # rotary: q and k of a packed (8, 2048, 3, 12, 64) bf16 qkv rotated in place;
+        # algorithmic bytes = read + write of q and k (the cos/sin rows stay in L2)
+        from flash_attn.rotary import RotaryEmbedding, apply_rotary_emb_qkv_
+        qkv_r = torch.randn(8, 2048, 3 * 12 * 64, generator=torch.Generator().manual_seed(5)).bfloat16().to(dev)
+        rc, rs = RotaryEmbedding(64).to(dev).cos_sin_tables(2048, dev, torch.bfloat16)
+        ms_r, _ = time_events(lambda: apply_rotary_emb_qkv_(qkv_r, rc, rs, 12, 64), 20, 3)
+        rbytes = 2 * 2 * 8 * 2048 * 12 * 64 * 2
+        extra["rotary_qkv_inplace_B8_S2048_H12_D64_bf16"] = {
+            "ms": round(ms_r, 4), "GBps": round(rbytes / ms_r / 1e6, 1), "frac_hbm": round(rbytes / ms_r / 1e6 / PEAK_HBM_GBS, 4)}
+        del qkv_r
         # C3 forward + backward (the fwd+bwd headline of the reference README charts)
         q3, k3, v3, _, c3q, c3k = make_inputs(8, 12, 2048, 2048, 64, torch.bfloat16, dev)
         q3.requires_grad_(); k3.requires_grad_(); v3.requires_grad_()

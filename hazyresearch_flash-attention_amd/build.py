@@ -19,7 +19,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 BUILD = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "flash_attn", "libfa_hip.so")
 
-SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_padding.hip", "fa_d32.hip", "fa_d64.hip", "fa_d128.hip"]
+SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_padding.hip", "fa_rotary.hip", "fa_d32.hip", "fa_d64.hip", "fa_d128.hip"]
 ARCH = os.environ.get("FA_OFFLOAD_ARCH", "gfx950")
 
 

@@ -82,6 +82,7 @@ int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {
         case FA_QUERY_BWD_ARGS_SIZE: return (int64_t)sizeof(FaBwdArgs);
         case FA_QUERY_MASK_ARGS_SIZE: return (int64_t)sizeof(FaBlockMask);
         case FA_QUERY_PAD_WORKSPACE: return a * (int64_t)sizeof(int32_t);
+        case FA_QUERY_ROTARY_ARGS_SIZE: return (int64_t)sizeof(FaRotaryArgs);
         default: return -1;
     }
 }
@@ -245,6 +246,29 @@ int fa_index_add_first_axis(const void *src, int64_t src_row_stride, const int64
     hipError_t e = fa::launch_scatter_add_rows(src, src_row_stride, indices, n, dst, dst_rows, dst_row_stride,
                                                row_elems, dtype, (hipStream_t)stream);
     return e == hipSuccess ? FA_OK : hip_fail(e, "fa_index_add_first_axis launch");
+}
+
+// ---- rotary embedding
+int fa_rotary(const FaRotaryArgs *a, void *stream) {
+    g_last_error.clear();
+    if (a == nullptr) return fail(FA_ERR_INVALID_ARGUMENT, "fa_rotary: args is NULL");
+    if (a->dtype != FA_DTYPE_FP16 && a->dtype != FA_DTYPE_BF16)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_rotary: dtype must be fp16 or bf16");
+    if (a->batch < 0 || a->seqlen < 0 || a->nslot < 0 || a->nheads < 0 || a->nrot < 0 || a->nrot > a->nslot)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_rotary: negative size or nrot > nslot");
+    if (a->head_dim <= 0 || a->head_dim % 8 != 0)
+        return fail(FA_ERR_UNSUPPORTED, "fa_rotary: head_dim must be a positive multiple of 8 (got %d)", a->head_dim);
+    if ((int64_t)a->batch * a->seqlen * a->nslot * a->nheads == 0) return FA_OK;
+    if (!a->x || !a->y || (a->nrot > 0 && (!a->cos || !a->sin)))
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_rotary: NULL pointer");
+    int64_t m = a->table_stride;
+    for (int i = 0; i < 4; ++i) m |= a->x_strides[i] | a->y_strides[i];
+    if (m % 8 != 0 || !aligned16(a->x) || !aligned16(a->y) || (a->nrot > 0 && (!aligned16(a->cos) || !aligned16(a->sin))))
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_rotary: tensors must be 16-byte aligned with strides multiple of 8");
+    if (a->nrot > 0 && a->table_stride < a->head_dim)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_rotary: table_stride < head_dim");
+    hipError_t e = fa::launch_rotary(*a, (hipStream_t)stream);
+    return e == hipSuccess ? FA_OK : hip_fail(e, "fa_rotary launch");
 }
 
 }  // extern "C"

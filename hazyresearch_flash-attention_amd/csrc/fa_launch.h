@@ -16,6 +16,7 @@ hipError_t launch_pad_rows(const void *src, int64_t src_stride, const int64_t *i
 hipError_t launch_scatter_add_rows(const void *src, int64_t src_stride, const int64_t *idx, int64_t n, void *dst,
                                    int64_t dst_rows, int64_t dst_stride, int64_t elems_per_row, int dtype,
                                    hipStream_t s);
+hipError_t launch_rotary(const FaRotaryArgs &a, hipStream_t s);
 hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t stream);
 hipError_t launch_bwd_post(const FaBwdArgs &a, hipStream_t stream);
 }  // namespace fa

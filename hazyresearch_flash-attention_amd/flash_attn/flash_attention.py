@@ -9,7 +9,7 @@ import torch.nn as nn
 
 from flash_attn.bert_padding import pad_input, unpad_input
 from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func
-from flash_attn.rotary import RotaryEmbedding, RotaryEmbedding2D
+from flash_attn.rotary import RotaryEmbedding, RotaryEmbedding2D, apply_rotary_emb_qkv_
 
 
 class FlashAttention(nn.Module):
@@ -81,8 +81,12 @@ class FlashMHA(nn.Module):
         """x: (batch, seqlen, embed_dim); key_padding_mask: (batch, seqlen) bool."""
         qkv = self.Wqkv(x)
         b, s = qkv.shape[0], qkv.shape[1]
+        if self.use_rotary_emb and qkv.is_cuda and qkv.is_contiguous():
+            # q and k rotated in place in the packed projection (fa_rotary): no unbind/stack copies
+            cos, sin = self.rotary_emb.cos_sin_tables(s, qkv.device, qkv.dtype)
+            qkv = apply_rotary_emb_qkv_(qkv, cos, sin, self.num_heads, self.head_dim)
         qkv = qkv.reshape(b, s, 3, self.num_heads, self.head_dim)
-        if self.use_rotary_emb:
+        if self.use_rotary_emb and not qkv.is_cuda:
             q, k, v = qkv.unbind(dim=2)
             q, k = self.rotary_emb(q, k, seq_dimension=-3)
             qkv = torch.stack([q, k, v], dim=2)

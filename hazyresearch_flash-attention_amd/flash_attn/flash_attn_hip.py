@@ -28,6 +28,7 @@ FA_QUERY_FWD_ARGS_SIZE = 4
 FA_QUERY_BWD_ARGS_SIZE = 5
 FA_QUERY_MASK_ARGS_SIZE = 6
 FA_QUERY_PAD_WORKSPACE = 7
+FA_QUERY_ROTARY_ARGS_SIZE = 8
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -82,6 +83,14 @@ class FaBlockMask(ctypes.Structure):
     _fields_ = [("mask", _vp), ("row_stride", _i64), ("rows", _i32), ("cols", _i32)]
 
 
+class FaRotaryArgs(ctypes.Structure):
+    """ctypes mirror of FaRotaryArgs (include/fa_hip.h)."""
+    _fields_ = [("x", _vp), ("y", _vp), ("cos", _vp), ("sin", _vp),
+                ("x_strides", _i64 * 4), ("y_strides", _i64 * 4), ("table_stride", _i64),
+                ("batch", _i32), ("seqlen", _i32), ("nslot", _i32), ("nheads", _i32), ("head_dim", _i32),
+                ("nrot", _i32), ("inverse", _i32), ("dtype", _i32)]
+
+
 _lib_handle = None
 
 
@@ -108,6 +117,8 @@ def lib():
         h.fa_index_put_first_axis.restype = ctypes.c_int
         h.fa_index_add_first_axis.argtypes = [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp]
         h.fa_index_add_first_axis.restype = ctypes.c_int
+        h.fa_rotary.argtypes = [ctypes.POINTER(FaRotaryArgs), _vp]
+        h.fa_rotary.restype = ctypes.c_int
         h.fa_query.argtypes = [ctypes.c_int, _i64, _i64, _i64]
         h.fa_query.restype = _i64
         h.fa_last_error.argtypes = []
@@ -118,6 +129,8 @@ def lib():
             raise ImportError("FaFwdArgs layout mismatch between fa_hip.h and flash_attn_hip.py")
         if h.fa_query(FA_QUERY_BWD_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaBwdArgs):
             raise ImportError("FaBwdArgs layout mismatch between fa_hip.h and flash_attn_hip.py")
+        if h.fa_query(FA_QUERY_ROTARY_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaRotaryArgs):
+            raise ImportError("FaRotaryArgs layout mismatch between fa_hip.h and flash_attn_hip.py")
         if h.fa_query(FA_QUERY_MASK_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaBlockMask):
             raise ImportError("FaBlockMask layout mismatch between fa_hip.h and flash_attn_hip.py")
         _lib_handle = h
@@ -368,3 +381,25 @@ def bwd_block(dout, qkv, out, S_dmask, softmax_lse, cu_seqlens, blockmask, p_dro
                     cu_seqlens, cu_seqlens, max_s, max_s, p_dropout, softmax_scale, False, is_causal, gen,
                     rng_state=rng_state, layout=layout)
     return dqkv, None, softmax_d
+
+
+def rotary(x, y, cos, sin, shape, x_strides, y_strides, nrot, inverse):
+    """fa_rotary over the (B, S, NSLOT, H, D) views of x and y given by `shape` and element
+    strides (batch, seq, slot, head); y may be x (in place)."""
+    B, S, NS, H, D = shape
+    a = FaRotaryArgs()
+    a.x, a.y = x.data_ptr(), y.data_ptr()
+    a.cos, a.sin = cos.data_ptr(), sin.data_ptr()
+    for i in range(4):
+        a.x_strides[i] = int(x_strides[i])
+        a.y_strides[i] = int(y_strides[i])
+    a.table_stride = cos.stride(0)
+    a.batch, a.seqlen, a.nslot, a.nheads, a.head_dim = B, S, NS, H, D
+    a.nrot, a.inverse = nrot, 1 if inverse else 0
+    a.dtype = _dtype_code(x.dtype)
+    _check(cos.stride(0) == sin.stride(0), "cos and sin tables must share a row stride")
+    with _on_device(x.device):
+        rc = lib().fa_rotary(ctypes.byref(a), _stream_ptr(x.device))
+    if rc != 0:
+        _raise(rc, "fa_rotary")
+    return y

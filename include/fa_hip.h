@@ -18,6 +18,8 @@
  *                              (flash_attn/bert_padding.py:41-55, 25-38); with unpad_input /
  *                              pad_input (:99-134) on top
  *   fa_index_add_first_axis <- IndexFirstAxisResidual.backward (flash_attn/bert_padding.py:82-94)
+ *   fa_rotary               <- apply_rotary_pos_emb + RotaryEmbedding(2D).forward and their autograd
+ *                              backward (flash_attn/rotary.py:22-41, 86-135)
  *   fa_query, fa_last_error, fa_version: host helpers (no reference counterpart; the reference
  *                                                  raised through TORCH_CHECK / exit(1),
  *                                                  fmha_api.cpp:131-170, fmha_utils.h:36-48)
@@ -162,6 +164,27 @@ int fa_index_add_first_axis(const void *src, int64_t src_row_stride, const int64
                             int64_t dst_rows, int64_t dst_row_stride, int64_t row_elems, int32_t dtype,
                             void *stream);
 
+/* Rotary position embedding (flash_attn/rotary.py:22-41): y = x*cos + rotate_half(x)*sin with
+ * interleaved pairs (2i, 2i+1), every product and the sum rounded to the 16-bit dtype as torch's
+ * eager evaluation does (bit-identical to the reference). inverse = 1 applies the autograd
+ * transpose (the backward). x, y: (B, S, NSLOT, H, D), element strides, stride(-1) == 1, 16-byte
+ * aligned rows; y may alias x. Slots [0, nrot) are rotated; the others are copied when y != x.
+ * cos/sin: (>= S, D) tables in x's dtype (position = index along S). */
+typedef struct FaRotaryArgs {
+    const void *x;
+    void *y;
+    const void *cos;
+    const void *sin;
+    int64_t x_strides[4];     /* batch, seq, slot, head (elements) */
+    int64_t y_strides[4];
+    int64_t table_stride;     /* elements between table rows */
+    int32_t batch, seqlen, nslot, nheads, head_dim;
+    int32_t nrot;
+    int32_t inverse;
+    int32_t dtype;            /* FA_DTYPE_FP16 / FA_DTYPE_BF16 */
+} FaRotaryArgs;
+int fa_rotary(const FaRotaryArgs *args, void *stream);
+
 enum {
     FA_QUERY_BWD_WORKSPACE = 1,   /* a = total_q, b = nheads, c = head_dim -> bytes */
     FA_QUERY_MAX_HEAD_DIM = 2,    /* -> 128 */
@@ -170,6 +193,7 @@ enum {
     FA_QUERY_BWD_ARGS_SIZE = 5,   /* sizeof(FaBwdArgs) */
     FA_QUERY_MASK_ARGS_SIZE = 6,  /* sizeof(FaBlockMask) */
     FA_QUERY_PAD_WORKSPACE = 7,   /* a = dst_rows -> bytes of fa_index_put_first_axis's workspace */
+    FA_QUERY_ROTARY_ARGS_SIZE = 8,   /* sizeof(FaRotaryArgs) */
 };
 int64_t fa_query(int what, int64_t a, int64_t b, int64_t c);
 

@@ -21,7 +21,7 @@ def _declared_functions():
 def test_header_declares_the_entry_points():
     assert _declared_functions() == ["fa_bwd", "fa_bwd_block", "fa_fwd", "fa_fwd_block", "fa_index_add_first_axis",
                                      "fa_index_first_axis", "fa_index_put_first_axis", "fa_last_error", "fa_query",
-                                     "fa_version"]
+                                     "fa_rotary", "fa_version"]
 
 
 def test_library_exports_every_declared_symbol():
@@ -37,6 +37,7 @@ def test_struct_layouts_match():
     assert L.fa_query(hip.FA_QUERY_FWD_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaFwdArgs)
     assert L.fa_query(hip.FA_QUERY_BWD_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaBwdArgs)
     assert L.fa_query(hip.FA_QUERY_MASK_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaBlockMask)
+    assert L.fa_query(hip.FA_QUERY_ROTARY_ARGS_SIZE, 0, 0, 0) == ctypes.sizeof(hip.FaRotaryArgs)
     assert L.fa_query(hip.FA_QUERY_MAX_HEAD_DIM, 0, 0, 0) == 128
     assert L.fa_query(hip.FA_QUERY_BWD_WORKSPACE, 10, 2, 64) == 10 * 2 * 64 * 4
     assert L.fa_query(999, 0, 0, 0) == -1

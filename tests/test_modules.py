@@ -60,8 +60,11 @@ def _mha_ref(mha, x, key_padding_mask, causal):
     from oracle.attention_ref import attention_ref
     qkv = mha.Wqkv(x).reshape(x.shape[0], x.shape[1], 3, mha.num_heads, mha.head_dim)
     q, k, v = qkv.unbind(dim=2)
-    if mha.use_rotary_emb:
-        q, k = mha.rotary_emb(q, k, seq_dimension=-3)
+    if mha.use_rotary_emb:   # the torch expression on the host (fresh module, same tables)
+        from flash_attn.rotary import RotaryEmbedding, RotaryEmbedding2D
+        emb = (RotaryEmbedding if mha.use_rotary_emb == "1d" else RotaryEmbedding2D)(mha.head_dim)
+        qc, kc = emb(q.detach().cpu(), k.detach().cpu(), seq_dimension=-3)
+        q, k = qc.to(q.device), kc.to(k.device)
     outs = []
     for up in (True, False):
         o, _ = attention_ref(q, k, v, key_padding_mask, key_padding_mask, causal=causal, upcast=up, reorder_ops=not up)
