@@ -28,6 +28,9 @@ namespace fa {
 // causal uses 4: smaller key blocks balance the triangular work better.
 template <bool CAUSAL>
 struct BwdWaves { static constexpr int value = CAUSAL ? 4 : 8; };
+// D=128: 4 waves (one per SIMD), so each wave may hold 512 registers (VGPR + AGPR)
+template <int D, bool CAUSAL>
+struct BwdWavesD { static constexpr int value = D == 128 ? 4 : BwdWaves<CAUSAL>::value; };
 
 template <int D, int NW_ = 8>
 struct BwdCfg {
@@ -113,13 +116,13 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
 #define FA_BWD_MINW 2   // __launch_bounds__ minimum waves per SIMD (2: two workgroups per CU when causal)
 #endif
 #if FA_BWD_MINW > 0
-#define FA_BWD_BOUNDS(C) __launch_bounds__(64 * BwdWaves<C>::value, FA_BWD_MINW)
+#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWavesD<D, C>::value), (D == 128 ? 1 : FA_BWD_MINW))
 #else
-#define FA_BWD_BOUNDS(C) __launch_bounds__(64 * BwdWaves<C>::value)
+#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWavesD<D, C>::value))
 #endif
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false>
 __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaBlockMask bm) {
-    using C = BwdCfg<D, BwdWaves<CAUSAL>::value>;
+    using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];

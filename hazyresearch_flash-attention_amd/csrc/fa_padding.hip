@@ -23,6 +23,10 @@ template <> struct Word<16> { typedef uint4 type; };
 template <> struct Word<4> { typedef uint32_t type; };
 template <> struct Word<2> { typedef uint16_t type; };
 
+// Each thread moves UNR words spaced one block apart (all loads issued before the stores, so a
+// wave keeps UNR KiB in flight).
+constexpr int UNR = 4;
+
 // dst[i][c] = src[idx[i]][c]; rows outside [0, src_rows) read as zeros
 template <int W>
 __global__ __launch_bounds__(256) void gather_rows_kernel(const char *__restrict__ src, int64_t src_rows,
@@ -30,13 +34,27 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const char *__restrict
                                                           int64_t n, char *__restrict__ dst, int64_t dst_stride,
                                                           int64_t words_per_row) {
     typedef typename Word<W>::type T;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * words_per_row) return;
-    const int64_t i = t / words_per_row, c = t - i * words_per_row;
-    const int64_t r = idx[i];
-    T v{};
-    if (r >= 0 && r < src_rows) v = *reinterpret_cast<const T *>(src + r * src_stride + c * W);
-    *reinterpret_cast<T *>(dst + i * dst_stride + c * W) = v;
+    const int64_t total = n * words_per_row;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * UNR + threadIdx.x;
+    T v[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+        const int64_t t = t0 + (int64_t)u * blockDim.x;
+        v[u] = T{};
+        if (t < total) {
+            const int64_t i = t / words_per_row, c = t - i * words_per_row;
+            const int64_t r = idx[i];
+            if (r >= 0 && r < src_rows) v[u] = *reinterpret_cast<const T *>(src + r * src_stride + c * W);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+        const int64_t t = t0 + (int64_t)u * blockDim.x;
+        if (t < total) {
+            const int64_t i = t / words_per_row, c = t - i * words_per_row;
+            *reinterpret_cast<T *>(dst + i * dst_stride + c * W) = v[u];
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void inverse_index_kernel(const int64_t *__restrict__ idx, int64_t n,
@@ -54,13 +72,27 @@ __global__ __launch_bounds__(256) void pad_rows_kernel(const char *__restrict__ 
                                                        char *__restrict__ dst, int64_t dst_stride,
                                                        int64_t words_per_row) {
     typedef typename Word<W>::type T;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= dst_rows * words_per_row) return;
-    const int64_t r = t / words_per_row, c = t - r * words_per_row;
-    const int32_t i = inv[r];
-    T v{};
-    if (i >= 0) v = *reinterpret_cast<const T *>(src + (int64_t)i * src_stride + c * W);
-    *reinterpret_cast<T *>(dst + r * dst_stride + c * W) = v;
+    const int64_t total = dst_rows * words_per_row;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * UNR + threadIdx.x;
+    T v[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+        const int64_t t = t0 + (int64_t)u * blockDim.x;
+        v[u] = T{};
+        if (t < total) {
+            const int64_t r = t / words_per_row, c = t - r * words_per_row;
+            const int32_t i = inv[r];
+            if (i >= 0) v[u] = *reinterpret_cast<const T *>(src + (int64_t)i * src_stride + c * W);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+        const int64_t t = t0 + (int64_t)u * blockDim.x;
+        if (t < total) {
+            const int64_t r = t / words_per_row, c = t - r * words_per_row;
+            *reinterpret_cast<T *>(dst + r * dst_stride + c * W) = v[u];
+        }
+    }
 }
 
 // dst[idx[i]][e] += src[i][e] (indices unique, as unpad_input produces them)
@@ -104,7 +136,7 @@ hipError_t launch_gather_rows(const void *src, int64_t src_rows, int64_t src_str
     const int w = word_size(src, dst, src_stride, dst_stride, row_bytes);
     const int64_t wpr = row_bytes / w;
     if (n * wpr == 0) return hipSuccess;
-    const dim3 grid(blocks_for(n * wpr));
+    const dim3 grid(blocks_for((n * wpr + UNR - 1) / UNR));
     const char *sp = (const char *)src;
     char *dp = (char *)dst;
     if (w == 16)
@@ -124,7 +156,7 @@ hipError_t launch_pad_rows(const void *src, int64_t src_stride, const int64_t *i
     if (n > 0) hipLaunchKernelGGL(inverse_index_kernel, dim3(blocks_for(n)), dim3(256), 0, s, idx, n, inv, dst_rows);
     const int w = word_size(src, dst, src_stride, dst_stride, row_bytes);
     const int64_t wpr = row_bytes / w;
-    const dim3 grid(blocks_for(dst_rows * wpr));
+    const dim3 grid(blocks_for((dst_rows * wpr + UNR - 1) / UNR));
     const char *sp = (const char *)src;
     char *dp = (char *)dst;
     if (w == 16)
