@@ -135,6 +135,23 @@ __device__ __forceinline__ u32x4 gload128(const void *p) { return *reinterpret_c
 __device__ __forceinline__ void gstore64(void *p, u32x2 v) { *reinterpret_cast<u32x2 *>(p) = v; }
 __device__ __forceinline__ void gstore128(void *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
 
+// Buffer descriptors (T8/T20): 32-bit per-lane offsets against a wave-uniform base, hardware
+// bounds check; an offset of OOB reads zeros / drops the store or atomic, so edge handling needs
+// no branches (and the compiler can count outstanding memory operations exactly).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload128(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+constexpr int OOB = (int)0x80000000;  // any offset past num_records reads as zero
+__device__ __forceinline__ float bload32f(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ void batomic_add(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
+    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, byte_off, 0, 0);
+}
+
 // Max over the lane pair (l, l^32) with v_permlane32_swap (T12).
 __device__ __forceinline__ float pair_max(float x) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);

@@ -77,13 +77,6 @@ struct FwdCfg {
 // log2-domain threshold of the deferred rescale: P values stay below 2^RESCALE_THR.
 constexpr float RESCALE_THR = 8.0f;
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7FFFFFFF, 0x00020000);
-}
-__device__ __forceinline__ u32x4 bload128(__amdgpu_buffer_rsrc_t r, int byte_off) {
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
-}
-constexpr int OOB = (int)0x80000000;  // any offset past num_records reads as zero
 
 // v_max3_f32 as one instruction (plain fmaxf at -O3 adds NaN-canonicalising v_max x,x first).
 __device__ __forceinline__ float max3f(float a, float b, float c) {

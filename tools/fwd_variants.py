@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "sparse_wpe1": {"FA_FWD_SPARSE_WPE": 1},
+    "bwd_minw1": {"FA_BWD_MINW": 1},
 }
 
 CONFIGS = [
