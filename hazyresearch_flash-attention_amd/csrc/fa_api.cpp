@@ -151,11 +151,6 @@ int bwd_impl(const FaBwdArgs *a, const FaBlockMask &bm, void *stream) {
          a->dv_head_stride) % 8 != 0)
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: tensors must be 16-byte aligned with strides multiple of 8");
     if (a->total_q < 0) return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: total_q < 0");
-    // per-sequence 32-bit buffer offsets: q/dO rows and the fp32 dQ workspace
-    const int64_t lim = (int64_t)1 << 31;
-    if ((int64_t)a->max_seqlen_q * a->q_row_stride * 2 >= lim || (int64_t)a->max_seqlen_q * a->do_row_stride * 2 >= lim ||
-        (int64_t)a->max_seqlen_q * a->nheads * a->head_dim * 4 >= lim)
-        return fail(FA_ERR_UNSUPPORTED, "fa_bwd: a sequence spans more than 2 GiB (seqlen * row_stride)");
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = fa::launch_bwd_pre(*a, s);
     if (e != hipSuccess) return hip_fail(e, "fa_bwd pre launch");

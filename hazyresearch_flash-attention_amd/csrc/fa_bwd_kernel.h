@@ -22,16 +22,12 @@
 #include "fa_common.h"
 #include "../../include/fa_hip.h"
 
-#ifndef FA_BWD_CAUSAL_NW
-#define FA_BWD_CAUSAL_NW 4   // waves (x32 keys) per causal backward workgroup
-#endif
-
 namespace fa {
 
 // Waves per workgroup (32 keys each). dQ atomic bytes scale with 1/NW, so non-causal uses 8;
 // causal uses 4: smaller key blocks balance the triangular work better.
 template <bool CAUSAL>
-struct BwdWaves { static constexpr int value = CAUSAL ? FA_BWD_CAUSAL_NW : 8; };
+struct BwdWaves { static constexpr int value = CAUSAL ? 4 : 8; };
 // D=128: 4 waves (one per SIMD), so each wave may hold 512 registers (VGPR + AGPR)
 template <int D, bool CAUSAL>
 struct BwdWavesD { static constexpr int value = D == 128 ? 4 : BwdWaves<CAUSAL>::value; };
@@ -116,9 +112,6 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
     gstore128((uint16_t *)a.dq + row * a.dq_row_stride + h * a.dq_head_stride + c * 8, w);
 }
 
-#ifndef FA_BWD_NO_ATOMIC
-#define FA_BWD_NO_ATOMIC 0
-#endif
 #ifndef FA_BWD_MINW
 #define FA_BWD_MINW 2   // __launch_bounds__ minimum waves per SIMD (2: two workgroups per CU when causal)
 #endif
@@ -171,15 +164,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     const float *lse_g = a.softmax_lse + (int64_t)(b * a.nheads + h) * a.lse_stride;
     const float *del_g = a.softmax_d + (int64_t)(b * a.nheads + h) * a.lse_stride;
     float *dqa = a.dq_accum + ((int64_t)q_start * a.nheads + h) * head_dim;
-    const int dqa_row = a.nheads * head_dim;
-    // buffer descriptors for everything touched per query tile: 32-bit offsets, no branches, so
-    // the compiler counts outstanding loads/atomics exactly (no vmcnt(0) behind the dQ atomics)
-    const auto qr = make_rsrc(qp);
-    const auto dor = make_rsrc(dop);
-    const auto lser = make_rsrc(lse_g);
-    const auto delr = make_rsrc(del_g);
-    const auto dqr = make_rsrc(dqa);
-    const int q_rs = (int)a.q_row_stride, do_rs = (int)a.do_row_stride;
+    const int64_t dqa_row = (int64_t)a.nheads * head_dim;
 
     // ---- stage the K block image (B operand of dQ = dS K, transposed reads)
     for (int idx = tid; idx < C::BKV * C::NC; idx += C::NT) {
@@ -234,13 +219,16 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             const int idx = tid + C::NT * i;
             const int row = idx / C::NC, c = idx % C::NC;
             const int q = q0n + row;
+            const u32x4 z = {0u, 0u, 0u, 0u};
             const bool ok = idx < C::BQ * C::NC && q < seqlen_q && c * 8 < head_dim;
-            qst[i] = bload128(qr, ok ? (q * q_rs + c * 8) * 2 : OOB);
-            dst[i] = bload128(dor, ok ? (q * do_rs + c * 8) * 2 : OOB);
+            qst[i] = ok ? gload128(qp + (int64_t)q * a.q_row_stride + c * 8) : z;
+            dst[i] = ok ? gload128(dop + (int64_t)q * a.do_row_stride + c * 8) : z;
         }
-        const int q = q0n + (tid % C::BQ);
-        lse_st = bload32f(lser, q < seqlen_q ? q * 4 : OOB) * LOG2E;
-        del_st = bload32f(delr, q < seqlen_q ? q * 4 : OOB);
+        if (tid < C::BQ) {
+            const int q = q0n + tid;
+            lse_st = q < seqlen_q ? lse_g[q] * LOG2E : 0.f;
+            del_st = q < seqlen_q ? del_g[q] : 0.f;
+        }
     };
     auto lds_store_qtile = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
@@ -400,11 +388,6 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             for (int g = 0; g < 4; ++g) lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), z);
         }
         __syncthreads();
-        // The next tile's Q/dO go into the other buffer now, before this tile's dQ atomics: its
-        // loads are older than the atomics, so waiting for them does not wait for the atomics
-        // (vmcnt counts loads and atomics in one ordered counter). The other buffer was last read
-        // in the previous step, before the barrier above.
-        if (itn < nqt) lds_store_qtile(1 - BUF);
 
         // ---- dQ[q][d] += dS[q][key] K[key][d] over the BKV keys (16x16x32 MFMAs); the
         // 2*(D/16) output tiles of 16 query rows x 16 columns are dealt round-robin to the waves,
@@ -428,18 +411,16 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                     acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
                 }
                 const int d = dbase + (lane & 15);
+                if (d < head_dim) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int q = q0 + 16 * qh + 4 * g4 + i;
-                    const bool ok = q < seqlen_q && d < head_dim;
-#if FA_BWD_NO_ATOMIC   // timing experiment only: drops dQ (wrong results)
-                    if (ok && acc[i] == 12345.f) dqa[(int64_t)q * dqa_row + d] = acc[i];
-#else
-                    batomic_add(dqr, ok ? (q * dqa_row + d) * 4 : OOB, acc[i]);
-#endif
+                    for (int i = 0; i < 4; ++i) {
+                        const int q = q0 + 16 * qh + 4 * g4 + i;
+                        if (q < seqlen_q) atomicAdd(dqa + (int64_t)q * dqa_row + d, acc[i]);
+                    }
                 }
             }
         }
+        if (itn < nqt) lds_store_qtile(1 - BUF);
         __syncthreads();
     };
     if constexpr (SPARSE) {

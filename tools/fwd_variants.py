@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "bwd_minw1": {"FA_BWD_MINW": 1},
+    "pingpong": {"FA_FWD_PINGPONG": 1},
 }
 
 CONFIGS = [
@@ -143,9 +143,82 @@ def run(names, rounds, iters):
     return results
 
 
+BWD_CONFIGS = [
+    # name, B, H, S, D, causal, p
+    ("bwd_ns_B8_H12_S2048_D64", 8, 12, 2048, 64, False, 0.0),
+    ("bwd_c3_B8_H12_S2048_D64_causal_p0.1", 8, 12, 2048, 64, True, 0.1),
+    ("bwd_ns_B8_H12_S2048_D128", 8, 12, 2048, 128, False, 0.0),
+]
+
+
+def run_bwd(names, rounds, iters):
+    """Interleaved A/B of fa_bwd (pre-pass + main + convert) per variant library."""
+    import torch
+    from flash_attn import flash_attn_hip as hip
+    libs = {}
+    for n in names:
+        L = ctypes.CDLL(os.path.join(BUILD, f"var_{n}.so"))
+        L.fa_bwd.argtypes = [ctypes.POINTER(hip.FaBwdArgs), ctypes.c_void_p]
+        L.fa_bwd.restype = ctypes.c_int
+        libs[n] = L
+    results = {}
+    for (cname, B, H, S, D, causal, p) in BWD_CONFIGS:
+        g = torch.Generator().manual_seed(0)
+        q, k, v, do = (torch.randn(B * S, H, D, generator=g).bfloat16().cuda() for _ in range(4))
+        cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device="cuda")
+        rng = (1234, 0)
+        o, lse = hip.fwd(q, k, v, cu, cu, S, S, p, D ** -0.5, False, causal, False, None, rng_state=rng)[:2]
+        dq_ref, dk_ref, dv_ref = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        hip.bwd(do, q, k, v, o, lse, dq_ref, dk_ref, dv_ref, cu, cu, S, S, p, D ** -0.5, False, causal, None,
+                rng_state=rng)
+        sd = torch.empty(B, H, lse.shape[2], dtype=torch.float32, device="cuda")
+        acc = torch.empty(B * S, H, D, dtype=torch.float32, device="cuda")
+        outs = {n: (torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)) for n in names}
+        a = hip.FaBwdArgs()
+        a.dout, a.q, a.k, a.v, a.out = do.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
+        a.softmax_lse, a.softmax_d, a.dq_accum = lse.data_ptr(), sd.data_ptr(), acc.data_ptr()
+        a.cu_seqlens_q = a.cu_seqlens_k = cu.data_ptr()
+        for f in ("do", "q", "k", "v", "o", "dq", "dk", "dv"):
+            setattr(a, f"{f}_row_stride", H * D)
+            setattr(a, f"{f}_head_stride", D)
+        a.batch, a.nheads, a.head_dim, a.max_seqlen_q, a.max_seqlen_k = B, H, D, S, S
+        a.total_q, a.lse_stride = B * S, lse.shape[2]
+        a.softmax_scale, a.p_dropout, a.rng_seed, a.rng_offset = D ** -0.5, p, rng[0], rng[1]
+        a.is_causal, a.dtype = int(causal), hip.FA_DTYPE_BF16
+        stream = torch.cuda.current_stream().cuda_stream
+        times = {n: [] for n in names}
+        flops = 2.5 * 4.0 * B * H * S * S * D / (2 if causal else 1)
+        for r in range(rounds):
+            for n in names:
+                dq, dk, dv = outs[n]
+                a.dq, a.dk, a.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+                L = libs[n]
+                for _ in range(2):
+                    L.fa_bwd(ctypes.byref(a), stream)
+                s = torch.cuda.Event(enable_timing=True)
+                e = torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(iters):
+                    rc = L.fa_bwd(ctypes.byref(a), stream)
+                e.record()
+                torch.cuda.synchronize()
+                assert rc == 0
+                times[n].append(s.elapsed_time(e) / iters)
+        res = {}
+        for n in names:
+            ts = sorted(times[n])
+            dq, dk, dv = outs[n]
+            err = max((x.float() - y.float()).abs().max().item() for x, y in ((dq, dq_ref), (dk, dk_ref), (dv, dv_ref)))
+            res[n] = {"ms_med": round(ts[len(ts) // 2], 4), "ms_min": round(ts[0], 4),
+                      "TFLOPS_med": round(flops / ts[len(ts) // 2] / 1e9, 1), "max_diff_vs_main": err}
+        results[cname] = res
+        print(cname, json.dumps(res), flush=True)
+    return results
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["build", "run"])
+    ap.add_argument("mode", choices=["build", "run", "runbwd"])
     ap.add_argument("--only", default="")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
@@ -154,7 +227,7 @@ if __name__ == "__main__":
     if args.mode == "build":
         build(names)
     else:
-        out = run(names, args.rounds, args.iters)
+        out = run(names, args.rounds, args.iters) if args.mode == "run" else run_bwd(names, args.rounds, args.iters)
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         with open(os.path.join(ROOT, "gpurun_out", "variants.json"), "w") as f:
             json.dump(out, f, indent=1)
