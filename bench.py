@@ -243,6 +243,26 @@ def main():
         extra["c3_B8_H12_S2048_D64_bf16_causal_p0.1_fwd_bwd"] = {
             "ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2), "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
 
+    if not args.no_extra and rank == 0:
+        # the reference's published metric (README.md:69-81): fwd+bwd speedup over PyTorch standard
+        # attention at B=8 H=12 D=64 fp16, S=2048, no mask / no dropout (tools/speedup_vs_pytorch.py
+        # sweeps S and the mask/dropout cases into profiles/)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from speedup_vs_pytorch import torch_attention, timed
+        from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func
+        qkv_s = torch.randn(8, 2048, 3, 12, 64, device=dev, dtype=torch.float16, requires_grad=True)
+        go_s = torch.randn(8, 2048, 12, 64, device=dev, dtype=torch.float16)
+        msk = torch.ones(8, 2048, dtype=torch.bool, device=dev)
+        qkv_u = qkv_s.detach().reshape(8 * 2048, 3, 12, 64).requires_grad_()
+        cu_s = torch.arange(0, 9 * 2048, 2048, dtype=torch.int32, device=dev)
+        t_f = timed(lambda: torch.autograd.grad(flash_attn_unpadded_qkvpacked_func(qkv_u, cu_s, 2048, 0.0), (qkv_u,),
+                                                go_s.reshape(8 * 2048, 12, 64)))
+        t_t = timed(lambda: torch.autograd.grad(torch_attention(qkv_s, msk, 0.0), (qkv_s,), go_s))
+        extra["fwd_bwd_speedup_vs_pytorch_B8_H12_S2048_D64_fp16"] = {
+            "flash_ms": round(t_f, 4), "pytorch_ms": round(t_t, 4), "speedup": round(t_t / t_f, 2),
+            "reference_A100_chart": 2.05}
+        del qkv_s, qkv_u
+
     cpu = None
     if not args.no_cpu and rank == 0 and world == 1:
         cpu = cpu_baseline(B, H, S, D)
