@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "pingpong": {"FA_FWD_PINGPONG": 1},
+    "bwd_minw1": {"FA_BWD_MINW": 1},
 }
 
 CONFIGS = [
