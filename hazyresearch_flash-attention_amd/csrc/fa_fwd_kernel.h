@@ -48,6 +48,9 @@ namespace fa {
 #ifndef FA_FWD_PINGPONG
 #define FA_FWD_PINGPONG 0  // 1: two half-workgroups half a tile apart (matrix/VALU phases paired)
 #endif
+#ifndef FA_FWD_WIDE_STORE
+#define FA_FWD_WIDE_STORE 1  // epilogue: 16-byte O stores via v_permlane32_swap (0: 8-byte stores)
+#endif
 #ifndef FA_FWD_SPARSE_WPE
 #define FA_FWD_SPARSE_WPE 4   // block-sparse kernels without dropout: register budget for 4 waves/SIMD
 #endif
@@ -562,6 +565,24 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
     if (DROPOUT) inv *= 1.0f / (1.0f - a.p_dropout);
     if (qrow < seqlen_q) {
         uint16_t *op = (uint16_t *)a.o + (int64_t)(q_start + qrow) * a.o_row_stride + (int64_t)h * a.o_head_stride;
+#if FA_FWD_WIDE_STORE
+        // 16-byte stores (T21): lanes l and l+32 hold the two 8-byte halves of each 8-column group
+        // of the same row; one v_permlane32_swap per word gives lane l group g4 whole and lane
+        // l+32 group g4+1 whole, so each lane writes 16 contiguous bytes instead of 2 x 8.
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; g4 += 2) {
+                const uint32_t a0 = T::pack2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+                const uint32_t a1 = T::pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+                const uint32_t b0 = T::pack2(o[dt][4 * g4 + 4] * inv, o[dt][4 * g4 + 5] * inv);
+                const uint32_t b1 = T::pack2(o[dt][4 * g4 + 6] * inv, o[dt][4 * g4 + 7] * inv);
+                const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+                const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+                const int d = 32 * dt + 8 * (g4 + hi);
+                if (d < head_dim) gstore128(op + d, u32x4{s0[0], s1[0], s0[1], s1[1]});
+            }
+#else
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -573,6 +594,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
                     gstore64(op + d, w);
                 }
             }
+#endif
         if (hi == 0) {
             a.softmax_lse[(int64_t)(b * a.nheads + h) * a.lse_stride + qrow] =
                 empty ? -INFINITY : m_i * a.softmax_scale + __logf(l_tot);

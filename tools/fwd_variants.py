@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "bwd_minw1": {"FA_BWD_MINW": 1},
+    "narrow_store": {"FA_FWD_WIDE_STORE": 0},
 }
 
 CONFIGS = [
