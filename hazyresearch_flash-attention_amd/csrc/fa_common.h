@@ -141,8 +141,15 @@ __device__ __forceinline__ void gstore128(void *p, u32x4 v) { *reinterpret_cast<
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7FFFFFFF, 0x00020000);
 }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_n(const void *base, int num_bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, num_bytes, 0x00020000);
+}
 __device__ __forceinline__ u32x4 bload128(__amdgpu_buffer_rsrc_t r, int byte_off) {
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+// lane offset + wave-uniform (SGPR) offset: the per-tile advance costs no vector instruction
+__device__ __forceinline__ u32x4 bload128s(__amdgpu_buffer_rsrc_t r, int byte_off, int soff) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, soff, 0));
 }
 constexpr int OOB = (int)0x80000000;  // any offset past num_records reads as zero
 __device__ __forceinline__ float bload32f(__amdgpu_buffer_rsrc_t r, int byte_off) {

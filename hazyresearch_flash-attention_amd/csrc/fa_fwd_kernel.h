@@ -54,6 +54,15 @@ namespace fa {
 #ifndef FA_FWD_SPARSE_WPE
 #define FA_FWD_SPARSE_WPE 4   // block-sparse kernels without dropout: register budget for 4 waves/SIMD
 #endif
+#ifndef FA_FWD_SOFF
+#define FA_FWD_SOFF 1      // 1: K/V tile loads = lane-constant offset + scalar tile offset; rows past the
+#endif                     //    end are cut by the buffer's record count (no per-tile vector bounds math)
+#ifndef FA_FWD_MTHR
+#define FA_FWD_MTHR 1      // 1: rescale test = one compare against a per-row threshold kept as state
+#endif
+#ifndef FA_FWD_DENSE_WPE
+#define FA_FWD_DENSE_WPE 4   // 8-wave dense D<=64 kernels without dropout: minimum waves per SIMD (2 workgroups per CU)
+#endif
 #ifndef FA_FWD_LDS_PAD
 #define FA_FWD_LDS_PAD 0   // extra LDS bytes per workgroup (caps workgroups per CU; experiments)
 #endif
@@ -101,6 +110,11 @@ __device__ __forceinline__ float max_tree32(const f32x16 &a, const f32x16 &b) {
     }
     return max3f(max3f(acc[0], acc[1], acc[2]), acc[3], acc[3]);
 }
+// max over the lane pair (l, l^32): one v_permlane32_swap and one v_max3 (no canonicalising v_max)
+__device__ __forceinline__ float pair_max3(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return max3f(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[1]));
+}
 __device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
     float t[16];
 #pragma unroll
@@ -119,10 +133,12 @@ __device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
 #endif
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
-__global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPOUT ? FA_FWD_SPARSE_WPE : 1))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
+__global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPOUT ? FA_FWD_SPARSE_WPE : (NW == 8 && D <= 64 && !DROPOUT ? FA_FWD_DENSE_WPE : 1)))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
     using C = FwdCfg<D, NW>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
+    constexpr float LN2 = 0.6931471805599453f;
+    constexpr bool MTHR = FA_FWD_MTHR && !SPARSE;   // measured slower on the block-sparse walk
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     // ---- block -> (q-block, head, batch)
@@ -164,12 +180,15 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
     const int head_dim = a.head_dim;
 
     const auto qr = make_rsrc((const uint16_t *)a.q + (int64_t)q_start * a.q_row_stride + (int64_t)h * a.q_head_stride);
-    const auto kr = make_rsrc((const uint16_t *)a.k + (int64_t)k_start * a.k_row_stride + (int64_t)h * a.k_head_stride);
-    const auto vr = make_rsrc((const uint16_t *)a.v + (int64_t)k_start * a.v_row_stride + (int64_t)h * a.v_head_stride);
-
     int n_end = seqlen_k;
     if (CAUSAL) n_end = min(n_end, q0 + C::BM);
     const int nt = (n_end + C::BN - 1) / C::BN;
+
+    // SOFF: the K/V descriptors end at row n_end, so rows past it read as zeros by themselves
+    const uint16_t *kbase = (const uint16_t *)a.k + (int64_t)k_start * a.k_row_stride + (int64_t)h * a.k_head_stride;
+    const uint16_t *vbase = (const uint16_t *)a.v + (int64_t)k_start * a.v_row_stride + (int64_t)h * a.v_head_stride;
+    const auto kr = FA_FWD_SOFF ? make_rsrc_n(kbase, n_end * (int)a.k_row_stride * 2) : make_rsrc(kbase);
+    const auto vr = FA_FWD_SOFF ? make_rsrc_n(vbase, n_end * (int)a.v_row_stride * 2) : make_rsrc(vbase);
 
     // ---- block sparsity (fa_fwd_block): this lane's live 256-key column blocks, and their union
     // over the workgroup's rows, which drives the tile walk (dead columns are never loaded)
@@ -218,7 +237,8 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
     for (int ks = 0; ks < D / 16; ++ks) {
         const int c = 2 * ks + hi;
         const bool ok = qrow < seqlen_q && c * 8 < head_dim;
-        qf[ks] = as_frag<T>(bload128(qr, ok ? (qrow * (int)a.q_row_stride + c * 8) * 2 : OOB));
+        u32x4 w = bload128(qr, ok ? (qrow * (int)a.q_row_stride + c * 8) * 2 : OOB);
+        qf[ks] = as_frag<T>(w);
     }
 
     // ---- register staging of K/V tiles (issue early, write late: T14). Loads are bounds-checked
@@ -232,6 +252,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
         st_okc[i] = c * 8 < head_dim;
         st_off_k[i] = (row * (int)a.k_row_stride + c * 8) * 2;
         st_off_v[i] = (row * (int)a.v_row_stride + c * 8) * 2;
+        if (FA_FWD_SOFF && !(st_okc[i] && idx < C::BN * C::NC)) st_off_k[i] = st_off_v[i] = OOB;
         st_lds[i] = S::off(row, c);
     }
     const int k_tile_step = C::BN * (int)a.k_row_stride * 2;
@@ -240,15 +261,23 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
     auto gload_k = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < C::CPT; ++i) {
-            const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
-            kst[i] = bload128(kr, ok ? st_off_k[i] + j * k_tile_step : OOB);
+            if (FA_FWD_SOFF) {
+                kst[i] = bload128s(kr, st_off_k[i], j * k_tile_step);
+            } else {
+                const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
+                kst[i] = bload128(kr, ok ? st_off_k[i] + j * k_tile_step : OOB);
+            }
         }
     };
     auto gload_v = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < C::CPT; ++i) {
-            const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
-            vst[i] = bload128(vr, ok ? st_off_v[i] + j * v_tile_step : OOB);
+            if (FA_FWD_SOFF) {
+                vst[i] = bload128s(vr, st_off_v[i], j * v_tile_step);
+            } else {
+                const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
+                vst[i] = bload128(vr, ok ? st_off_v[i] + j * v_tile_step : OOB);
+            }
         }
     };
     auto lds_store_k = [&](char *kb) __attribute__((always_inline)) {
@@ -273,6 +302,9 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
 #pragma unroll
     for (int r = 0; r < 16; ++r) lsum[r] = 0.f;
     const float c_log2 = a.softmax_scale * LOG2E;
+    const float thr_raw = RESCALE_THR / c_log2;
+    float m_thr = -INFINITY;   // MTHR: rescale when a tile max passes this (m + thr_raw)
+    float mc_row = 0.f;        // MTHR: m * c_log2 (0 before the first key)
 
     // dropout constants
     const uint32_t keep_thr = (uint32_t)floorf((1.0f - a.p_dropout) * 65535.0f);
@@ -317,57 +349,9 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
         }
     };
 
-    // ---- softmax of one tile in registers: mask, max, deferred rescale, exp, row sum,
-    // dropout, and conversion into the 16-bit B operand of P·V.
-    auto softmax_tile = [&](f32x16 (&s)[2], int kv0, typename T::frag (&pf)[2][2]) __attribute__((always_inline)) {
-        const bool dead = SPARSE && !((lane_cols >> (kv0 >> 8)) & 1);   // row's block is 0 in the layout
-        const bool need_mask = (kv0 + C::BN > seqlen_k) || (CAUSAL && kv0 + C::BN - 1 > qw) ||
-                               (SPARSE && __builtin_amdgcn_ballot_w64(dead));
-        if (need_mask) {
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int kv = kv0 + 32 * st + crow(r, hi);
-                    if (dead || kv >= seqlen_k || (CAUSAL && kv > qrow)) s[st][r] = -INFINITY;
-                }
-        }
-        const float mx = pair_max(max_tree32(s[0], s[1]));
-        const float m_new = fmaxf(m_i, mx);
-        const bool grow = (m_new - m_i) * c_log2 > RESCALE_THR;   // NaN (all -inf) -> false
-        if (__builtin_amdgcn_ballot_w64(grow)) {
-            const float alpha = grow ? fast_exp2((m_i - m_new) * c_log2) : 1.f;
-            if (grow) m_i = m_new;
-            l_i *= alpha;
-            if (FA_FWD_MFMA_SUM)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
-#pragma unroll
-            for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-        }
-        const float mc = (m_i == -INFINITY ? 0.f : m_i) * c_log2;
-        if (FA_FWD_PKFMA) {
-            typedef float f32x2 __attribute__((ext_vector_type(2)));
-            const f32x2 cc = {c_log2, c_log2}, mm = {-mc, -mc};
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                    f32x2 x = {s[st][r], s[st][r + 1]};
-                    x = __builtin_elementwise_fma(x, cc, mm);
-                    s[st][r] = fast_exp2(x[0]);
-                    s[st][r + 1] = fast_exp2(x[1]);
-                }
-        } else {
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
-        }
-        if (!FA_FWD_MFMA_SUM) l_i += sum_tree32(s[0], s[1]);
-
+    // ---- dropout (keep mask from the Philox stream) and conversion of P into the 16-bit B
+    // operand of P·V
+    auto dropout_cvt = [&](f32x16 (&s)[2], int kv0, typename T::frag (&pf)[2][2]) __attribute__((always_inline)) {
         if (DROPOUT) {
             // Keep mask generated in the column-major (backward) layout, transposed through a
             // per-wave LDS image with ds_read_b64_tr_b16.
@@ -408,6 +392,84 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
                 for (int e = 0; e < 4; ++e) pk[e] = T::pack2(s[st][8 * s2 + 2 * e], s[st][8 * s2 + 2 * e + 1]);
                 pf[st][s2] = as_frag<T>(pk);
             }
+    };
+
+    // ---- softmax of one tile in registers: mask, max, deferred rescale, exp, row sum,
+    // dropout, and conversion into the 16-bit B operand of P·V.
+    auto softmax_tile = [&](f32x16 (&s)[2], int kv0, typename T::frag (&pf)[2][2]) __attribute__((always_inline)) {
+        const bool dead = SPARSE && !((lane_cols >> (kv0 >> 8)) & 1);   // row's block is 0 in the layout
+        const bool need_mask = (kv0 + C::BN > seqlen_k) || (CAUSAL && kv0 + C::BN - 1 > qw) ||
+                               (SPARSE && __builtin_amdgcn_ballot_w64(dead));
+        if (need_mask) {
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int kv = kv0 + 32 * st + crow(r, hi);
+                    if (dead || kv >= seqlen_k || (CAUSAL && kv > qrow)) s[st][r] = -INFINITY;
+                }
+        }
+        const float mx = pair_max3(max_tree32(s[0], s[1]));
+        float mc;
+        if (MTHR) {
+            // m_thr = m + 2^RESCALE_THR in raw units (-inf before the first key); mc_row = m * c
+            const bool grow = mx > m_thr;   // NaN (all -inf) -> false
+            if (__builtin_amdgcn_ballot_w64(grow)) {
+                // m itself is not kept: alpha and the LSE only need m * c_log2
+                const float mcx = mx * c_log2;
+                const float alpha = grow ? fast_exp2(m_thr == -INFINITY ? -INFINITY : mc_row - mcx) : 1.f;
+                if (grow) {
+                    m_thr = mx + thr_raw;
+                    mc_row = mcx;
+                }
+                l_i *= alpha;
+                if (FA_FWD_MFMA_SUM)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            }
+            mc = mc_row;
+        } else {
+            const float m_new = fmaxf(m_i, mx);
+            const bool grow = (m_new - m_i) * c_log2 > RESCALE_THR;   // NaN (all -inf) -> false
+            if (__builtin_amdgcn_ballot_w64(grow)) {
+                const float alpha = grow ? fast_exp2((m_i - m_new) * c_log2) : 1.f;
+                if (grow) m_i = m_new;
+                l_i *= alpha;
+                if (FA_FWD_MFMA_SUM)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            }
+            mc = (m_i == -INFINITY ? 0.f : m_i) * c_log2;
+        }
+        if (FA_FWD_PKFMA) {
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            const f32x2 cc = {c_log2, c_log2}, mm = {-mc, -mc};
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                    f32x2 x = {s[st][r], s[st][r + 1]};
+                    x = __builtin_elementwise_fma(x, cc, mm);
+                    s[st][r] = fast_exp2(x[0]);
+                    s[st][r + 1] = fast_exp2(x[1]);
+                }
+        } else {
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
+        }
+        if (!FA_FWD_MFMA_SUM) l_i += sum_tree32(s[0], s[1]);
+
+        dropout_cvt(s, kv0, pf);
     };
 
     // ---- O^T += V^T P^T for one tile (and the optional all-ones row-sum MFMA)
@@ -597,7 +659,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
 #endif
         if (hi == 0) {
             a.softmax_lse[(int64_t)(b * a.nheads + h) * a.lse_stride + qrow] =
-                empty ? -INFINITY : m_i * a.softmax_scale + __logf(l_tot);
+                empty ? -INFINITY : (MTHR ? mc_row * LN2 : m_i * a.softmax_scale) + __logf(l_tot);
         }
     }
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include "fa_launch.h"
 #include "fa_fwd_kernel.h"
+#include "fa_fwd16_kernel.h"
 #include "fa_bwd_kernel.h"
 
 #include <cstdlib>
@@ -32,9 +33,27 @@ static int pick_fwd_waves(const FaFwdArgs &) {
     return (forced == 2 || forced == 4) ? forced : 8;
 }
 
+// Dense forward without dropout on 16x16x32 MFMA tiles (fa_fwd16_kernel.h), 8 waves.
+template <int D, typename T, bool CAUSAL>
+static hipError_t launch_fwd16(const FaFwdArgs &a, hipStream_t stream) {
+    using C = FwdCfg<D, 8>;
+    const int lds = C::lds_bytes(false);
+    auto kern = fa_fwd16_kernel<D, T, CAUSAL, 8>;
+    static const hipError_t attr_err =
+        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (attr_err != hipSuccess) return attr_err;
+    dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
+    hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a);
+    return hipGetLastError();
+}
+
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
 static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     if (bm.mask) return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8, true>(a, bm, stream);
+    if constexpr (!DROPOUT && FA_FWD16) {
+        // one lane offset serves the K and V tile loads there, so the row strides must agree
+        if (pick_fwd_waves(a) == 8 && a.k_row_stride == a.v_row_stride) return launch_fwd16<D, T, CAUSAL>(a, stream);
+    }
     switch (pick_fwd_waves(a)) {
         case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
         case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, bm, stream);

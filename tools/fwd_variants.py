@@ -22,7 +22,9 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "narrow_store": {"FA_FWD_WIDE_STORE": 0},
+    "mma32": {"FA_FWD16": 0},
+    "mma32_nomthr": {"FA_FWD16": 0, "FA_FWD_MTHR": 0},
+    "orig": {"FA_FWD16": 0, "FA_FWD_SOFF": 0, "FA_FWD_MTHR": 0, "FA_FWD_DENSE_WPE": 1},
 }
 
 CONFIGS = [
