@@ -112,6 +112,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
     gstore128((uint16_t *)a.dq + row * a.dq_row_stride + h * a.dq_head_stride + c * 8, w);
 }
 
+#ifndef FA_BWD_BQLOAD
+#define FA_BWD_BQLOAD 1   // 1: query-tile loads through buffer descriptors (32-bit lane offsets)
+#endif
 #ifndef FA_BWD_MINW
 #define FA_BWD_MINW 2   // __launch_bounds__ minimum waves per SIMD (2: two workgroups per CU when causal)
 #endif
@@ -213,16 +216,34 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     // the other half of the double-buffered Q/dO/lse/delta images.
     u32x4 qst[C::QCH], dst[C::QCH];
     float lse_st = 0.f, del_st = 0.f;
+    // BQLOAD: Q/dO tile loads as buffer loads, lane offset + scalar tile offset; the descriptors end
+    // at row seqlen_q, so rows past it read as zeros (32-bit lane offsets instead of 64-bit addresses)
+    const auto q_rs = make_rsrc_n(qp, seqlen_q * (int)a.q_row_stride * 2);
+    const auto do_rs = make_rsrc_n(dop, seqlen_q * (int)a.do_row_stride * 2);
+    int qld_off[C::QCH], dold_off[C::QCH];
+#pragma unroll
+    for (int i = 0; i < C::QCH; ++i) {
+        const int idx = tid + C::NT * i;
+        const int row = idx / C::NC, c = idx % C::NC;
+        const bool okc = idx < C::BQ * C::NC && c * 8 < head_dim;
+        qld_off[i] = okc ? (row * (int)a.q_row_stride + c * 8) * 2 : OOB;
+        dold_off[i] = okc ? (row * (int)a.do_row_stride + c * 8) * 2 : OOB;
+    }
     auto gload_qtile = [&](int q0n) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < C::QCH; ++i) {
-            const int idx = tid + C::NT * i;
-            const int row = idx / C::NC, c = idx % C::NC;
-            const int q = q0n + row;
-            const u32x4 z = {0u, 0u, 0u, 0u};
-            const bool ok = idx < C::BQ * C::NC && q < seqlen_q && c * 8 < head_dim;
-            qst[i] = ok ? gload128(qp + (int64_t)q * a.q_row_stride + c * 8) : z;
-            dst[i] = ok ? gload128(dop + (int64_t)q * a.do_row_stride + c * 8) : z;
+            if (FA_BWD_BQLOAD) {
+                qst[i] = bload128s(q_rs, qld_off[i], q0n * (int)a.q_row_stride * 2);
+                dst[i] = bload128s(do_rs, dold_off[i], q0n * (int)a.do_row_stride * 2);
+            } else {
+                const int idx = tid + C::NT * i;
+                const int row = idx / C::NC, c = idx % C::NC;
+                const int q = q0n + row;
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                const bool ok = idx < C::BQ * C::NC && q < seqlen_q && c * 8 < head_dim;
+                qst[i] = ok ? gload128(qp + (int64_t)q * a.q_row_stride + c * 8) : z;
+                dst[i] = ok ? gload128(dop + (int64_t)q * a.do_row_stride + c * 8) : z;
+            }
         }
         if (tid < C::BQ) {
             const int q = q0n + tid;

@@ -12,9 +12,10 @@
 // MI355X-first structure (NOT the reference's FA-1 loop order): FA-2 order, grid =
 // (q-blocks, H, B) remapped so that all q-blocks of one head run on one XCD (its K/V stay in
 // that XCD's L2). A workgroup = 8 waves = 256 query rows, one wave = 32 rows. Q stays in VGPRs;
-// K/V tiles of 64 keys are loaded with bounds-checked buffer loads (out-of-range -> 0, no
-// branches) into registers early and written late into a double-buffered, XOR-swizzled LDS
-// image (one barrier per tile). The loop is unrolled by two so every LDS address is a
+// K/V tiles of 64 keys go HBM -> LDS by LDS-DMA (buffer_load ... lds: each wave-instruction writes
+// 1 KiB of the image, the XOR swizzle is applied on the source address; bounds-checked, so rows
+// past the end and padded columns land as zeros) into a double-buffered image, one barrier per
+// tile (the block-sparse walk stages through registers). The loop is unrolled by two so every LDS address is a
 // lane-constant base plus an immediate. Scores are computed swapped (S^T = K Q^T,
 // v_mfma_f32_32x32x16) so each lane owns one query row: the row max is a tree of v_max3 plus one
 // v_permlane32_swap, the row sum stays lane-local until the epilogue, and P feeds the P·V MFMA
@@ -60,6 +61,9 @@ namespace fa {
 #ifndef FA_FWD_MTHR
 #define FA_FWD_MTHR 1      // 1: rescale test = one compare against a per-row threshold kept as state
 #endif
+#ifndef FA_FWD_DMA
+#define FA_FWD_DMA 1       // 1: dense K/V tiles staged by LDS-DMA (buffer_load ... lds, swizzle on the
+#endif                     //    source address) instead of registers + ds_write
 #ifndef FA_FWD_DENSE_WPE
 #define FA_FWD_DENSE_WPE 4   // 8-wave dense D<=64 kernels without dropout: minimum waves per SIMD (2 workgroups per CU)
 #endif
@@ -538,6 +542,51 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
     // Software pipeline (T15, FA_FWD_PIPE): while the VALU runs the softmax of tile j, the matrix
     // pipe computes S of tile j+1 (K one tile ahead of V in LDS). Plain: K[j], V[j] in buffer P.
     f32x16 sA[2], sB[2];   // S of even / odd tiles
+    // DMA: piece p (1 KiB = RPP rows of the tile image) is written by wave p % NW; lane l lands at
+    // byte 16 l of the piece, i.e. row RPP p + l / NC, slot l % NC, which holds chunk slot ^ x(row)
+    constexpr int PIECES = C::TILE_BYTES / 1024;
+    constexpr int PPW = (PIECES + NW - 1) / NW;
+    constexpr int RPP = 1024 / (2 * D);
+    int dma_k_off[PPW], dma_v_off[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int p = wave + NW * i;
+        const int r = RPP * p + lane / C::NC;
+        const int c = (lane % C::NC) ^ S::x(r);
+        const bool ok = c * 8 < head_dim;
+        dma_k_off[i] = ok ? (r * (int)a.k_row_stride + c * 8) * 2 : OOB;
+        dma_v_off[i] = ok ? (r * (int)a.v_row_stride + c * 8) * 2 : OOB;
+    }
+    auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, const int (&off)[PPW], int step_bytes, char *buf, int j)
+        __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            const int p = wave + NW * i;
+#if defined(__HIP_DEVICE_COMPILE__)   // (the host pass would drop the kernel's launch stub over it)
+            if (PIECES % NW == 0 || p < PIECES)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(buf + 1024 * p), 16,
+                                                         off[i], j * step_bytes, 0, 0);
+#endif
+        }
+    };
+    // stage the next K/V tiles: issue (loads) early, commit (LDS writes, or the DMA's wait) late
+    auto stage_issue = [&](char *kb_wr, char *vb_wr, int jk, int jv) __attribute__((always_inline)) {
+        if constexpr (FA_FWD_DMA) {
+            dma_tile(kr, dma_k_off, k_tile_step, kb_wr, jk);
+            dma_tile(vr, dma_v_off, v_tile_step, vb_wr, jv);
+        } else {
+            gload_k(jk);
+            gload_v(jv);
+        }
+    };
+    auto stage_commit = [&](char *kb_wr, char *vb_wr) __attribute__((always_inline)) {
+        if constexpr (FA_FWD_DMA) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            lds_store_k(kb_wr);
+            lds_store_v(vb_wr);
+        }
+    };
     auto step = [&](auto par_tag, int j) __attribute__((always_inline)) {
         constexpr int P = decltype(par_tag)::value;
         constexpr bool PIPE = FA_FWD_PIPE;
@@ -548,8 +597,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
         char *kb_wr = smem + (PIPE ? P : 1 - P) * C::TILE_BYTES;
         char *vb_wr = smem + (3 - P) * C::TILE_BYTES;
         const int kv0 = j * C::BN;
-        gload_k(PIPE ? j + 2 : j + 1);
-        gload_v(j + 1);
+        stage_issue(kb_wr, vb_wr, PIPE ? j + 2 : j + 1, j + 1);
         if constexpr (!PIPE) qk(kb_rd, s);
         typename T::frag pf[2][2];
         if constexpr (PIPE) {
@@ -558,8 +606,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
         }
         softmax_tile(s, kv0, pf);
         pv(vb_rd, pf);
-        lds_store_k(kb_wr);
-        lds_store_v(vb_wr);
+        stage_commit(kb_wr, vb_wr);
         __syncthreads();
     };
 
@@ -603,10 +650,8 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPO
         }
     } else {
         // prologue: K[0] -> kbuf0, V[0] -> vbuf0 (+ K[1] -> kbuf1 and S of tile 0 when pipelined)
-        gload_k(0);
-        gload_v(0);
-        lds_store_k(smem);
-        lds_store_v(smem + 2 * C::TILE_BYTES);
+        stage_issue(smem, smem + 2 * C::TILE_BYTES, 0, 0);
+        stage_commit(smem, smem + 2 * C::TILE_BYTES);
         if (FA_FWD_PIPE) {
             gload_k(1);
             lds_store_k(smem + C::TILE_BYTES);

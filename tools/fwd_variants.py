@@ -22,9 +22,10 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "mma32": {"FA_FWD16": 0},
-    "mma32_nomthr": {"FA_FWD16": 0, "FA_FWD_MTHR": 0},
-    "orig": {"FA_FWD16": 0, "FA_FWD_SOFF": 0, "FA_FWD_MTHR": 0, "FA_FWD_DENSE_WPE": 1},
+    "dma": {"FA_FWD_DMA": 1},
+    "dma_wpe2": {"FA_FWD_DMA": 1, "FA_FWD_DENSE_WPE": 2},
+    "bwd_minw1": {"FA_BWD_MINW": 1},
+    "bwd_noqload": {"FA_BWD_BQLOAD": 0},
 }
 
 CONFIGS = [
