@@ -130,6 +130,16 @@ __device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
     return t[0];
 }
 
+// Minimum waves per SIMD the register allocation must allow (waves/SIMD = 512 / registers):
+// 8-wave workgroups hold two waves per SIMD each, so 4 = two workgroups per CU (128 registers);
+// 4-wave workgroups hold one, so 4 / 3 / 2 = four / three / two workgroups per CU.
+constexpr int fwd_waves_per_eu(int D, int NW, bool dropout, bool sparse) {
+    return sparse && !dropout ? FA_FWD_SPARSE_WPE
+         : NW == 8            ? (D <= 64 && !dropout ? FA_FWD_DENSE_WPE : 1)
+         : NW == 4            ? (D <= 64 ? (dropout ? 3 : 4) : 2)
+                              : 1;
+}
+
 #if FA_FWD_WPS > 0
 #define FA_FWD_BOUNDS(NW) __launch_bounds__(64 * NW, FA_FWD_WPS)
 #else
@@ -137,7 +147,7 @@ __device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
 #endif
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
-__global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(SPARSE && !DROPOUT ? FA_FWD_SPARSE_WPE : (NW == 8 && D <= 64 && !DROPOUT ? FA_FWD_DENSE_WPE : 1)))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
+__global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu(D, NW, DROPOUT, SPARSE)))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
     using C = FwdCfg<D, NW>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;

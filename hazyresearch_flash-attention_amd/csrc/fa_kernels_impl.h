@@ -22,15 +22,22 @@ static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipSt
     return hipGetLastError();
 }
 
-// Waves per workgroup. 8 (256 query rows) measured fastest on every BASELINE config, including
-// the short S=512 one where fewer waves would spread over more CUs (344 vs 339 vs 331 TF/s for
-// 8/4/2). FA_FWD_NW=2|4|8 overrides it for tuning.
+#ifndef FA_FWD_NW_DEFAULT
+#define FA_FWD_NW_DEFAULT 8
+#endif
+// Waves per workgroup. 8 (256 query rows, two workgroups per CU at 128 registers) measured
+// fastest without dropout on every BASELINE config, including the short S=512 one (428 vs 420
+// TF/s for 8/4). With dropout the kernel needs ~168 registers: 8-wave workgroups then fit one per
+// CU (two waves per SIMD), 4-wave ones three per CU, and C3's forward runs 457 vs 369 TF/s.
+// FA_FWD_NW=2|4|8 overrides the choice for tuning.
+template <int D, bool DROPOUT>
 static int pick_fwd_waves(const FaFwdArgs &) {
     static const int forced = [] {
         const char *e = getenv("FA_FWD_NW");
         return e ? atoi(e) : 0;
     }();
-    return (forced == 2 || forced == 4) ? forced : 8;
+    if (forced == 2 || forced == 4 || forced == 8) return forced;
+    return DROPOUT && D <= 64 ? 4 : FA_FWD_NW_DEFAULT;
 }
 
 // Dense forward without dropout on 16x16x32 MFMA tiles (fa_fwd16_kernel.h), 8 waves.
@@ -52,9 +59,9 @@ static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStr
     if (bm.mask) return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8, true>(a, bm, stream);
     if constexpr (!DROPOUT && FA_FWD16) {
         // one lane offset serves the K and V tile loads there, so the row strides must agree
-        if (pick_fwd_waves(a) == 8 && a.k_row_stride == a.v_row_stride) return launch_fwd16<D, T, CAUSAL>(a, stream);
+        if (pick_fwd_waves<D, DROPOUT>(a) == 8 && a.k_row_stride == a.v_row_stride) return launch_fwd16<D, T, CAUSAL>(a, stream);
     }
-    switch (pick_fwd_waves(a)) {
+    switch (pick_fwd_waves<D, DROPOUT>(a)) {
         case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
         case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, bm, stream);
         default: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 2>(a, bm, stream);

@@ -22,10 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "dma": {"FA_FWD_DMA": 1},
-    "dma_wpe2": {"FA_FWD_DMA": 1, "FA_FWD_DENSE_WPE": 2},
-    "bwd_minw1": {"FA_BWD_MINW": 1},
-    "bwd_noqload": {"FA_BWD_BQLOAD": 0},
+    "nw4": {"FA_FWD_NW_DEFAULT": 4},
 }
 
 CONFIGS = [
@@ -34,6 +31,8 @@ CONFIGS = [
     ("c4_B16_H12_S4096_D128_causal", 16, 12, 4096, 4096, 128, True, "bf16"),
     ("c5_B4_H16_1024x4096_D64", 4, 16, 1024, 4096, 64, False, "bf16"),
     ("bs_localglobal_B8_H12_S2048_D64", 8, 12, 2048, 2048, 64, False, "bf16"),   # fa_fwd_block
+    ("c2_B8_H12_S512_D64_fp16", 8, 12, 512, 512, 64, False, "fp16"),
+    ("c3_B8_H12_S2048_D64_causal_p0.1", 8, 12, 2048, 2048, 64, True, "bf16", 0.1),
 ]
 
 
@@ -80,7 +79,8 @@ def run(names, rounds, iters):
         L.fa_fwd_block.restype = ctypes.c_int
         libs[n] = L
     results = {}
-    for (cname, B, H, Sq, Sk, D, causal, dt) in CONFIGS:
+    for (cname, B, H, Sq, Sk, D, causal, dt, *pdrop) in CONFIGS:
+        p = pdrop[0] if pdrop else 0.0
         dtype = torch.bfloat16 if dt == "bf16" else torch.float16
         g = torch.Generator().manual_seed(0)
         q = torch.randn(B * Sq, H, D, generator=g).to(dtype).cuda()
@@ -96,7 +96,8 @@ def run(names, rounds, iters):
             lay = (((rblk - cblk).abs() <= 1) | (cblk == 0)).to(torch.uint8).cuda()
             live = lay.float().mean().item()
             m, _keep = hip._mask_struct(lay, q.device)
-        ref, _lse = hip.fwd(q, k, v, cq, ck, Sq, Sk, 0.0, D ** -0.5, False, causal, False, None, layout=lay)
+        ref, _lse = hip.fwd(q, k, v, cq, ck, Sq, Sk, p, D ** -0.5, False, causal, False, None, layout=lay,
+                            rng_state=(1234, 0))
         outs = {}
         a = hip.FaFwdArgs()
         lse = torch.empty(B, H, (Sq + 15) // 16 * 16, dtype=torch.float32, device="cuda")
@@ -111,6 +112,7 @@ def run(names, rounds, iters):
         a.max_seqlen_q, a.max_seqlen_k, a.lse_stride = Sq, Sk, lse.shape[2]
         a.softmax_scale = D ** -0.5
         a.is_causal = 1 if causal else 0
+        a.p_dropout, a.rng_seed, a.rng_offset = p, 1234, 0
         a.dtype = hip.FA_DTYPE_BF16 if dt == "bf16" else hip.FA_DTYPE_FP16
         stream = torch.cuda.current_stream().cuda_stream
         for n in names:
