@@ -24,6 +24,10 @@
 
 namespace fa {
 
+#ifndef FA_BWD_KV_LDS
+#define FA_BWD_KV_LDS 1   // 1 (D <= 64, 4-wave blocks): K/V B operands re-read from LDS every query tile
+#endif
+
 // Waves per workgroup (32 keys each). dQ atomic bytes scale with 1/NW, so non-causal uses 8;
 // causal uses 4: smaller key blocks balance the triangular work better.
 template <bool CAUSAL>
@@ -50,7 +54,13 @@ struct BwdCfg {
     static constexpr int OFF_DELTA = OFF_LSE + 2 * BQ * 4;
     static constexpr int OFF_QLIVE = OFF_DELTA + 2 * BQ * 4;   // block-sparse: live query tiles, 1 bit each
     static constexpr int QLIVE_WORDS = 16;                      // <= 1024 tiles (32768 rows)
-    static constexpr int LDS_BYTES = OFF_QLIVE + QLIVE_WORDS * 8;
+    // KV_LDS: a V image beside the K image; K and V fragments are read from LDS per query tile
+    // instead of being held in 32 registers for the whole kernel. The 4-wave (causal) kernels
+    // spilled inside the loop without it (C3 backward 0.557 -> 0.398 ms); the 8-wave non-causal
+    // ones fit and lose 2 % with it.
+    static constexpr bool KV_LDS = FA_BWD_KV_LDS && D <= 64 && NW == 4;
+    static constexpr int OFF_V = OFF_QLIVE + QLIVE_WORDS * 8;
+    static constexpr int LDS_BYTES = OFF_V + (KV_LDS ? K_IMG : 0);
     static constexpr int QCH = (BQ * NC + NT - 1) / NT;   // staged 16-B chunks per thread per tile
 };
 
@@ -176,6 +186,11 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         u32x4 v = {0u, 0u, 0u, 0u};
         if (kv < seqlen_k && c * 8 < head_dim) v = gload128(kp + (int64_t)kv * a.k_row_stride + c * 8);
         lds_write128(kimg, S::off(row, c), v);
+        if constexpr (C::KV_LDS) {
+            u32x4 w = {0u, 0u, 0u, 0u};
+            if (kv < seqlen_k && c * 8 < head_dim) w = gload128(vp + (int64_t)kv * a.v_row_stride + c * 8);
+            lds_write128(smem + C::OFF_V, S::off(row, c), w);
+        }
     }
     // ---- K, V rows of this lane's key as B operands: B[k=d][col=key]
     typename T::frag kf[D / 16], vf[D / 16];
@@ -183,7 +198,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     for (int ks = 0; ks < D / 16; ++ks) {
         const int c = 2 * ks + hi;
         u32x4 kv4 = {0u, 0u, 0u, 0u}, vv4 = {0u, 0u, 0u, 0u};
-        if (kvrow < seqlen_k && c * 8 < head_dim) {
+        if (!C::KV_LDS && kvrow < seqlen_k && c * 8 < head_dim) {
             kv4 = gload128(kp + (int64_t)kvrow * a.k_row_stride + c * 8);
             vv4 = gload128(vp + (int64_t)kvrow * a.v_row_stride + c * 8);
         }
@@ -328,8 +343,14 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             for (int ks = 0; ks < D / 16; ++ks) {
                 u32x4 qa = lds_read128(qimg, S::off(l32, 2 * ks + hi));
                 u32x4 da = lds_read128(doimg, S::off(l32, 2 * ks + hi));
-                sacc = T::mfma32(as_frag<T>(qa), kf[ks], sacc);
-                zacc = T::mfma32(as_frag<T>(da), vf[ks], zacc);
+                if constexpr (C::KV_LDS) {
+                    const int ko = S::off(32 * wave + l32, 2 * ks + hi);
+                    sacc = T::mfma32(as_frag<T>(qa), as_frag<T>(lds_read128(kimg, ko)), sacc);
+                    zacc = T::mfma32(as_frag<T>(da), as_frag<T>(lds_read128(smem + C::OFF_V, ko)), zacc);
+                } else {
+                    sacc = T::mfma32(as_frag<T>(qa), kf[ks], sacc);
+                    zacc = T::mfma32(as_frag<T>(da), vf[ks], zacc);
+                }
             }
             // row constants for rows crow(4g+e, hi) = 8g + 4hi + e (16-B aligned groups of 4)
             const bool need_mask = (q0 + C::BQ > seqlen_q) || (k0 + C::BKV > seqlen_k) ||

@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "nw4": {"FA_FWD_NW_DEFAULT": 4},
+    "kvlds": {"FA_BWD_KV_LDS": 1},
 }
 
 CONFIGS = [
