@@ -8,14 +8,15 @@
 //     dV = Pd^T dO,  dZ = dO V^T,  delta = rowsum(dO*O),  dS = P * (dZ*M/pk - delta),
 //     dQ = scale * dS K,  dK = scale * dS^T Q.
 //
-// Structure (MI355X-first): grid = (key blocks of 128, H, B); a workgroup = 4 waves, one wave
-// owns 32 keys and keeps K, V (as MFMA B operands) and dK^T, dV^T accumulators in registers for
-// the whole kernel. It sweeps 32-row query tiles: Q and dO tiles are staged into swizzled LDS
+// Structure (MI355X-first): grid = (key blocks of 32 NW, H, B); a workgroup = NW waves (8 at
+// D <= 64, 4 at D = 128), one wave owns 32 keys and keeps its dK^T, dV^T accumulators in registers
+// for the whole kernel; its K, V rows (MFMA B operands) stay in registers too, or, in the causal
+// kernels, are re-read per query tile from LDS images. It sweeps 32-row query tiles: Q and dO tiles are staged into swizzled LDS
 // images that serve both row reads (S = Q K^T, dZ = dO V^T) and transposed reads
 // (dV^T += dO^T Pd, dK^T += Q^T dS). Scores are computed with the key on the MFMA lane, so
 // P/dS accumulators are already the B operands of dV^T/dK^T. dS crosses LDS once (a [key][query]
-// image) for dQ = dS K, computed with 16x16x32 MFMAs so each of the 4 waves owns whole dQ tiles
-// summed over all 128 keys, then added with fp32 atomics into a workspace; a last kernel scales
+// image) for dQ = dS K, computed with 16x16x32 MFMAs so each wave owns whole dQ tiles summed
+// over all the block's keys, then added with fp32 atomics into a workspace; a last kernel scales
 // and converts dQ into the (possibly strided) output.
 #pragma once
 
@@ -24,19 +25,28 @@
 
 namespace fa {
 
+#ifndef FA_BWD_CAUSAL_NW
+#define FA_BWD_CAUSAL_NW 8      // waves (32 keys each) per causal backward workgroup (8: C3 0.405 -> 0.366 ms vs 4)
+#endif
+#ifndef FA_BWD_NONCAUSAL_NW
+#define FA_BWD_NONCAUSAL_NW 8
+#endif
 #ifndef FA_BWD_KV_LDS
-#define FA_BWD_KV_LDS 1   // 1 (D <= 64, 4-wave blocks): K/V B operands re-read from LDS every query tile
+#define FA_BWD_KV_LDS 1         // 1 (D <= 64, causal): K/V B operands re-read from LDS every query tile
+#endif
+#ifndef FA_BWD_KV_LDS8
+#define FA_BWD_KV_LDS8 0        // 1: the same for the non-causal kernels (A/B: 2-5 % slower there)
 #endif
 
-// Waves per workgroup (32 keys each). dQ atomic bytes scale with 1/NW, so non-causal uses 8;
-// causal uses 4: smaller key blocks balance the triangular work better.
+// Waves per workgroup (32 keys each). dQ atomic bytes scale with 1/NW, so both use 8 at D <= 64
+// (causal: 4-wave blocks balanced the triangle better but were slower once K/V moved to LDS).
 template <bool CAUSAL>
-struct BwdWaves { static constexpr int value = CAUSAL ? 4 : 8; };
+struct BwdWaves { static constexpr int value = CAUSAL ? FA_BWD_CAUSAL_NW : FA_BWD_NONCAUSAL_NW; };
 // D=128: 4 waves (one per SIMD), so each wave may hold 512 registers (VGPR + AGPR)
 template <int D, bool CAUSAL>
 struct BwdWavesD { static constexpr int value = D == 128 ? 4 : BwdWaves<CAUSAL>::value; };
 
-template <int D, int NW_ = 8>
+template <int D, int NW_ = 8, bool CAUSAL_ = false>
 struct BwdCfg {
     static constexpr int NW = NW_;
     static constexpr int NT = 64 * NW;      // threads per workgroup
@@ -55,10 +65,10 @@ struct BwdCfg {
     static constexpr int OFF_QLIVE = OFF_DELTA + 2 * BQ * 4;   // block-sparse: live query tiles, 1 bit each
     static constexpr int QLIVE_WORDS = 16;                      // <= 1024 tiles (32768 rows)
     // KV_LDS: a V image beside the K image; K and V fragments are read from LDS per query tile
-    // instead of being held in 32 registers for the whole kernel. The 4-wave (causal) kernels
-    // spilled inside the loop without it (C3 backward 0.557 -> 0.398 ms); the 8-wave non-causal
-    // ones fit and lose 2 % with it.
-    static constexpr bool KV_LDS = FA_BWD_KV_LDS && D <= 64 && NW == 4;
+    // instead of being held in 32 registers for the whole kernel. The causal kernels (mask and
+    // LPT bookkeeping on top) spilled inside the loop without it (C3 backward 0.557 -> 0.398 ms
+    // on 4-wave blocks); the non-causal ones fit and lose 2-5 % with it.
+    static constexpr bool KV_LDS = FA_BWD_KV_LDS && D <= 64 && (CAUSAL_ || FA_BWD_KV_LDS8);
     static constexpr int OFF_V = OFF_QLIVE + QLIVE_WORDS * 8;
     static constexpr int LDS_BYTES = OFF_V + (KV_LDS ? K_IMG : 0);
     static constexpr int QCH = (BQ * NC + NT - 1) / NT;   // staged 16-B chunks per thread per tile
@@ -135,7 +145,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
 #endif
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false>
 __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaBlockMask bm) {
-    using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value>;
+    using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value, CAUSAL>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];

@@ -70,7 +70,7 @@ static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStr
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE>
 static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
-    using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value>;
+    using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value, CAUSAL>;
     auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT, SPARSE>;
     static const hipError_t attr_err =
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);

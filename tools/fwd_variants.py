@@ -22,7 +22,8 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "kvlds": {"FA_BWD_KV_LDS": 1},
+    "causal8": {"FA_BWD_CAUSAL_NW": 8, "FA_BWD_KV_LDS8": 1},
+    "nc4": {"FA_BWD_NONCAUSAL_NW": 4},
 }
 
 CONFIGS = [
