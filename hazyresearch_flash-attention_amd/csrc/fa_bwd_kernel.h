@@ -34,6 +34,9 @@ namespace fa {
 #ifndef FA_BWD_KV_LDS
 #define FA_BWD_KV_LDS 1         // 1 (D <= 64, causal): K/V B operands re-read from LDS every query tile
 #endif
+#ifndef FA_BWD_RAWROW
+#define FA_BWD_RAWROW 1         // 1: lse/delta row loads consumed only at the LDS write (no early vmcnt wait)
+#endif
 #ifndef FA_BWD_KV_LDS8
 #define FA_BWD_KV_LDS8 0        // 1: the same for the non-causal kernels (A/B: 2-5 % slower there)
 #endif
@@ -272,8 +275,17 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         }
         if (tid < C::BQ) {
             const int q = q0n + tid;
-            lse_st = q < seqlen_q ? lse_g[q] * LOG2E : 0.f;
-            del_st = q < seqlen_q ? del_g[q] : 0.f;
+            if (FA_BWD_RAWROW) {
+                // unconditional loads of a clamped row, used only at the LDS write: no wait on
+                // them (and on the tile loads issued before them) at the top of the step. Rows
+                // past seqlen_q are masked to P = 0 whatever their constants.
+                const int qc = min(q, seqlen_q - 1);
+                lse_st = lse_g[qc];
+                del_st = del_g[qc];
+            } else {
+                lse_st = q < seqlen_q ? lse_g[q] * LOG2E : 0.f;
+                del_st = q < seqlen_q ? del_g[q] : 0.f;
+            }
         }
     };
     auto lds_store_qtile = [&](int buf) __attribute__((always_inline)) {
@@ -287,7 +299,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             }
         }
         if (tid < C::BQ) {
-            lse_s[buf * C::BQ + tid] = lse_st;
+            lse_s[buf * C::BQ + tid] = FA_BWD_RAWROW ? lse_st * LOG2E : lse_st;
             del_s[buf * C::BQ + tid] = del_st;
         }
     };

@@ -22,8 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "causal8": {"FA_BWD_CAUSAL_NW": 8, "FA_BWD_KV_LDS8": 1},
-    "nc4": {"FA_BWD_NONCAUSAL_NW": 4},
+    "norawrow": {"FA_BWD_RAWROW": 0},
 }
 
 CONFIGS = [
