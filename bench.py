@@ -174,7 +174,7 @@ def main():
                 fn = lambda: flash_attn_unpadded_kvpacked_func(q_, kv_, cq, ck, Sq_, Sk_, p, causal=causal)
             else:
                 fn = lambda: flash_attn_unpadded_func(q_, k_, v_, cq, ck, Sq_, Sk_, p, causal=causal)
-            ms, _ = time_events(fn, 10, 3)
+            ms, _ = time_events(fn, 20, 60)   # warm-up long enough for the clock to ramp (~30 ms)
             fl = fwd_flops(B_, H_, Sq_, Sk_, D_, causal)
             extra[name] = {"ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2),
                            "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
@@ -194,7 +194,7 @@ def main():
         cblk = torch.arange(8)[None, :]
         lay = (((rblk - cblk).abs() <= 1) | (cblk == 0)).to(dev)
         live_frac = lay.float().mean().item()
-        ms, _ = time_events(lambda: flash_blocksparse_attn_func(qkv_bs, cu_bs, lay, 0.0, 2048), 10, 3)
+        ms, _ = time_events(lambda: flash_blocksparse_attn_func(qkv_bs, cu_bs, lay, 0.0, 2048), 20, 60)
         fl = fwd_flops(8, 12, 2048, 2048, 64, False) * live_frac
         extra["blocksparse_B8_H12_S2048_D64_bf16_local_global_fwd"] = {
             "ms": round(ms, 4), "live_fraction": round(live_frac, 4), "TFLOPS_live": round(fl / ms / 1e9, 2),
@@ -238,7 +238,7 @@ def main():
             o = flash_attn_unpadded_func(q3, k3, v3, c3q, c3k, 2048, 2048, 0.1, causal=True)
             torch.autograd.grad(o, (q3, k3, v3), gout)
 
-        ms, _ = time_events(fb, 5, 2)
+        ms, _ = time_events(fb, 10, 20)
         fl = fwd_flops(8, 12, 2048, 2048, 64, True) * 3.5
         extra["c3_B8_H12_S2048_D64_bf16_causal_p0.1_fwd_bwd"] = {
             "ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2), "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
