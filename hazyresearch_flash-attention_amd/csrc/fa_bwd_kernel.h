@@ -37,6 +37,9 @@ namespace fa {
 #ifndef FA_BWD_RAWROW
 #define FA_BWD_RAWROW 1         // 1: lse/delta row loads consumed only at the LDS write (no early vmcnt wait)
 #endif
+#ifndef FA_BWD_FULLTILE
+#define FA_BWD_FULLTILE 1       // 1: unguarded dQ atomics on full query tiles
+#endif
 #ifndef FA_BWD_KV_LDS8
 #define FA_BWD_KV_LDS8 0        // 1: the same for the non-causal kernels (A/B: 2-5 % slower there)
 #endif
@@ -475,7 +478,12 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                     acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
                 }
                 const int d = dbase + (lane & 15);
-                if (d < head_dim) {
+                if (FA_BWD_FULLTILE && q0 + C::BQ <= seqlen_q && head_dim == D) {
+                    // full tile (wave-uniform test): the four atomics without per-lane guards
+                    float *base = dqa + (int64_t)(q0 + 16 * qh + 4 * g4) * dqa_row + d;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) atomicAdd(base + i * dqa_row, acc[i]);
+                } else if (d < head_dim) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int q = q0 + 16 * qh + 4 * g4 + i;

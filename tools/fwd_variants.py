@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "norawrow": {"FA_BWD_RAWROW": 0},
+    "nofull": {"FA_BWD_FULLTILE": 0},
 }
 
 CONFIGS = [
