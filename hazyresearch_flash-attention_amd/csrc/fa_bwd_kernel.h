@@ -40,6 +40,9 @@ namespace fa {
 #ifndef FA_BWD_FULLTILE
 #define FA_BWD_FULLTILE 1       // 1: unguarded dQ atomics on full query tiles
 #endif
+#ifndef FA_BWD_DQ_PREFETCH
+#define FA_BWD_DQ_PREFETCH 1    // 1: dQ MFMA operands read one key step ahead
+#endif
 #ifndef FA_BWD_KV_LDS8
 #define FA_BWD_KV_LDS8 0        // 1: the same for the non-causal kernels (A/B: 2-5 % slower there)
 #endif
@@ -302,8 +305,10 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             }
         }
         if (tid < C::BQ) {
-            lse_s[buf * C::BQ + tid] = FA_BWD_RAWROW ? lse_st * LOG2E : lse_st;
-            del_s[buf * C::BQ + tid] = del_st;
+            // one lane offset for both rows' constants (the image offsets fold into the
+            // instruction), so no per-buffer address stays live across the loop
+            lds_write32(smem + C::OFF_LSE + buf * C::BQ * 4, 4 * tid, FA_BWD_RAWROW ? lse_st * LOG2E : lse_st);
+            lds_write32(smem + C::OFF_DELTA + buf * C::BQ * 4, 4 * tid, del_st);
         }
     };
     // ---- block sparsity (fa_bwd_block): this workgroup's keys lie in one 256-key column block
@@ -466,16 +471,33 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                 const int qh = t & 1;
                 const int dbase = 16 * (t >> 1);
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                auto dq_operands = [&](int ks, u32x4 &av, u32x4 &bv) __attribute__((always_inline)) {
                     const int r0 = 32 * ks + 8 * g4 + qq;
                     u32x2 a0 = lds_read_tr(dsimg, ds_off(r0, 16 * qh + 4 * pp));
                     u32x2 a1 = lds_read_tr(dsimg, ds_off(r0 + 4, 16 * qh + 4 * pp));
-                    u32x4 av = {a0[0], a0[1], a1[0], a1[1]};
+                    av = u32x4{a0[0], a0[1], a1[0], a1[1]};
                     u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
                     u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
-                    u32x4 bv = {b0[0], b0[1], b1[0], b1[1]};
-                    acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
+                    bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
+                };
+                if constexpr (FA_BWD_DQ_PREFETCH) {
+                    // operands of key step ks+1 are read before the MFMA of step ks
+                    u32x4 av, bv, avn, bvn;
+                    dq_operands(0, av, bv);
+#pragma unroll
+                    for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                        if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
+                        acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
+                        av = avn;
+                        bv = bvn;
+                    }
+                } else {
+#pragma unroll
+                    for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                        u32x4 av, bv;
+                        dq_operands(ks, av, bv);
+                        acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
+                    }
                 }
                 const int d = dbase + (lane & 15);
                 if (FA_BWD_FULLTILE && q0 + C::BQ <= seqlen_q && head_dim == D) {

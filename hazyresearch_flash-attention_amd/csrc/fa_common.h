@@ -118,6 +118,10 @@ __device__ __forceinline__ void lds_write128(char *lds, int byte_off, u32x4 v) {
     *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(
         (__attribute__((address_space(3))) char *)lds + byte_off) = v;
 }
+__device__ __forceinline__ void lds_write32(char *lds, int byte_off, float v) {
+    *reinterpret_cast<__attribute__((address_space(3))) float *>(
+        (__attribute__((address_space(3))) char *)lds + byte_off) = v;
+}
 __device__ __forceinline__ void lds_write64(char *lds, int byte_off, u32x2 v) {
     *reinterpret_cast<__attribute__((address_space(3))) u32x2 *>(
         (__attribute__((address_space(3))) char *)lds + byte_off) = v;

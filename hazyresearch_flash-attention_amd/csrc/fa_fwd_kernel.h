@@ -134,7 +134,7 @@ __device__ __forceinline__ float sum_tree32(const f32x16 &a, const f32x16 &b) {
 // 8-wave workgroups hold two waves per SIMD each, so 4 = two workgroups per CU (128 registers);
 // 4-wave workgroups hold one, so 4 / 3 / 2 = four / three / two workgroups per CU.
 constexpr int fwd_waves_per_eu(int D, int NW, bool dropout, bool sparse) {
-    return sparse && !dropout ? FA_FWD_SPARSE_WPE
+    return sparse && !dropout && D <= 64 ? FA_FWD_SPARSE_WPE
          : NW == 8            ? (D <= 64 && !dropout ? FA_FWD_DENSE_WPE : 1)
          : NW == 4            ? (D <= 64 ? (dropout ? 3 : 4) : 2)
                               : 1;

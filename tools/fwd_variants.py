@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "nofull": {"FA_BWD_FULLTILE": 0},
+    "nopf": {"FA_BWD_DQ_PREFETCH": 0},
 }
 
 CONFIGS = [
