@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "nopf": {"FA_BWD_DQ_PREFETCH": 0},
+    "nosplit": {"FA_BWD_SPLIT128": 0},
 }
 
 CONFIGS = [
