@@ -162,8 +162,10 @@ int bwd_impl(const FaBwdArgs *a, const FaBlockMask &bm, void *stream) {
         }
         if (e != hipSuccess) return hip_fail(e, "fa_bwd launch");
     }
-    e = fa::launch_bwd_post(*a, s);
-    if (e != hipSuccess) return hip_fail(e, "fa_bwd post launch");
+    if (!fa::bwd_dq_direct(*a, bm)) {
+        e = fa::launch_bwd_post(*a, s);
+        if (e != hipSuccess) return hip_fail(e, "fa_bwd post launch");
+    }
     return FA_OK;
 }
 

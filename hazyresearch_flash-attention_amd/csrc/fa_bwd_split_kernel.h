@@ -47,7 +47,8 @@ struct BwdSplitCfg {
     static constexpr int QCH = (BQ * NC + NT - 1) / NT;
 };
 
-template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false>
+// DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
+template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
 __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a, const FaBlockMask bm) {
     using C = BwdSplitCfg<D, CAUSAL>;
     using S = Swz<D>;
@@ -311,10 +312,12 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
                     }
                 }
                 // dS^T image: row = key (32*kwave + l32), columns = query rows 8g + 4hi .. +3
+                if constexpr (DQ) {
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    u32x2 w = {T::pack2(x[4 * g + 0], x[4 * g + 1]), T::pack2(x[4 * g + 2], x[4 * g + 3])};
-                    lds_write64(dsimg, ds_off(32 * kwave + l32, 8 * g + 4 * hi), w);
+                    for (int g = 0; g < 4; ++g) {
+                        u32x2 w = {T::pack2(x[4 * g + 0], x[4 * g + 1]), T::pack2(x[4 * g + 2], x[4 * g + 3])};
+                        lds_write64(dsimg, ds_off(32 * kwave + l32, 8 * g + 4 * hi), w);
+                    }
                 }
             }
             // ---- dV^T += dO^T Pd (P waves) or dK^T += Q^T dS (dS waves), A operands by transposed reads
@@ -333,49 +336,51 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
                     acc[dt] = T::mfma32(as_frag<T>(u32x4{a0[0], a0[1], a1[0], a1[1]}), as_frag<T>(pk), acc[dt]);
                 }
             }
-        } else if (!role_p) {
+        } else if (DQ && !role_p) {
             const u32x2 z = {0u, 0u};
 #pragma unroll
             for (int g = 0; g < 4; ++g) lds_write64(dsimg, ds_off(32 * kwave + l32, 8 * g + 4 * hi), z);
         }
-        __syncthreads();   // dS image complete
+        if constexpr (DQ) {
+            __syncthreads();   // dS image complete
 
-        // ---- dQ = dS K over the block's keys: 16x16x32 MFMAs, 2 x D/16 tiles dealt to the waves
-#pragma unroll
-        for (int t0 = 0; t0 < 2 * (D / 16); t0 += C::NW) {
-            const int t = t0 + wave;
-            if (t < 2 * (D / 16)) {
-                const int qh = t & 1;
-                const int dbase = 16 * (t >> 1);
-                f32x4 dacc = {0.f, 0.f, 0.f, 0.f};
-                auto dq_operands = [&](int ks, u32x4 &av, u32x4 &bv) __attribute__((always_inline)) {
-                    const int r0 = 32 * ks + 8 * g4 + qq;
-                    u32x2 a0 = lds_read_tr(dsimg, ds_off(r0, 16 * qh + 4 * pp));
-                    u32x2 a1 = lds_read_tr(dsimg, ds_off(r0 + 4, 16 * qh + 4 * pp));
-                    av = u32x4{a0[0], a0[1], a1[0], a1[1]};
-                    u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
-                    u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
-                    bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
-                };
-                u32x4 av, bv, avn, bvn;
-                dq_operands(0, av, bv);
-#pragma unroll
-                for (int ks = 0; ks < C::BKV / 32; ++ks) {
-                    if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
-                    dacc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), dacc);
-                    av = avn;
-                    bv = bvn;
-                }
-                const int d = dbase + (lane & 15);
-                if (q0 + C::BQ <= seqlen_q && head_dim == D) {
-                    float *base = dqa + (int64_t)(q0 + 16 * qh + 4 * g4) * dqa_row + d;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) atomicAdd(base + i * dqa_row, dacc[i]);
-                } else if (d < head_dim) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int q = q0 + 16 * qh + 4 * g4 + i;
-                        if (q < seqlen_q) atomicAdd(dqa + (int64_t)q * dqa_row + d, dacc[i]);
+            // ---- dQ = dS K over the block's keys: 16x16x32 MFMAs, 2 x D/16 tiles dealt to the waves
+    #pragma unroll
+            for (int t0 = 0; t0 < 2 * (D / 16); t0 += C::NW) {
+                const int t = t0 + wave;
+                if (t < 2 * (D / 16)) {
+                    const int qh = t & 1;
+                    const int dbase = 16 * (t >> 1);
+                    f32x4 dacc = {0.f, 0.f, 0.f, 0.f};
+                    auto dq_operands = [&](int ks, u32x4 &av, u32x4 &bv) __attribute__((always_inline)) {
+                        const int r0 = 32 * ks + 8 * g4 + qq;
+                        u32x2 a0 = lds_read_tr(dsimg, ds_off(r0, 16 * qh + 4 * pp));
+                        u32x2 a1 = lds_read_tr(dsimg, ds_off(r0 + 4, 16 * qh + 4 * pp));
+                        av = u32x4{a0[0], a0[1], a1[0], a1[1]};
+                        u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
+                        u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
+                        bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
+                    };
+                    u32x4 av, bv, avn, bvn;
+                    dq_operands(0, av, bv);
+    #pragma unroll
+                    for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                        if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
+                        dacc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), dacc);
+                        av = avn;
+                        bv = bvn;
+                    }
+                    const int d = dbase + (lane & 15);
+                    if (q0 + C::BQ <= seqlen_q && head_dim == D) {
+                        float *base = dqa + (int64_t)(q0 + 16 * qh + 4 * g4) * dqa_row + d;
+    #pragma unroll
+                        for (int i = 0; i < 4; ++i) atomicAdd(base + i * dqa_row, dacc[i]);
+                    } else if (d < head_dim) {
+    #pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int q = q0 + 16 * qh + 4 * g4 + i;
+                            if (q < seqlen_q) atomicAdd(dqa + (int64_t)q * dqa_row + d, dacc[i]);
+                        }
                     }
                 }
             }

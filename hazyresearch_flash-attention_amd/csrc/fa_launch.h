@@ -18,5 +18,17 @@ hipError_t launch_scatter_add_rows(const void *src, int64_t src_stride, const in
                                    hipStream_t s);
 hipError_t launch_rotary(const FaRotaryArgs &a, hipStream_t s);
 hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t stream);
+
+#ifndef FA_BWD_SPLIT128
+#define FA_BWD_SPLIT128 1   // 1: D = 128 backward with the P / dS wave split (fa_bwd_split_kernel.h)
+#endif
+#ifndef FA_BWD_DQK
+#define FA_BWD_DQK 1        // 1: D = 128 dense, no dropout: dQ by the query-major fa_bwd_dq_kernel
+#endif
+// true when launch_bwd writes dq itself (no fp32 accumulator, no convert pass)
+inline bool bwd_dq_direct(const FaBwdArgs &a, const FaBlockMask &bm) {
+    return FA_BWD_SPLIT128 && FA_BWD_DQK && a.head_dim > 64 && a.p_dropout == 0.f && bm.mask == nullptr &&
+           a.max_seqlen_k > 0;
+}
 hipError_t launch_bwd_post(const FaBwdArgs &a, hipStream_t stream);
 }  // namespace fa

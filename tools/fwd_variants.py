@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "nosplit": {"FA_BWD_SPLIT128": 0},
+    "nodqk": {"FA_BWD_DQK": 0},
 }
 
 CONFIGS = [
@@ -153,6 +153,7 @@ BWD_CONFIGS = [
     ("bwd_ns_B8_H12_S2048_D64", 8, 12, 2048, 64, False, 0.0),
     ("bwd_c3_B8_H12_S2048_D64_causal_p0.1", 8, 12, 2048, 64, True, 0.1),
     ("bwd_ns_B8_H12_S2048_D128", 8, 12, 2048, 128, False, 0.0),
+    ("bwd_c_B8_H12_S2048_D128_causal", 8, 12, 2048, 128, True, 0.0),
 ]
 
 
