@@ -152,7 +152,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
 #else
 #define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWavesD<D, C>::value))
 #endif
-template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false>
+// DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
+template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
 __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaBlockMask bm) {
     using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value, CAUSAL>;
     using S = Swz<D>;
@@ -448,68 +449,72 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                 }
             }
             // ---- dS^T image: row = key (32*wave + l32), columns = query rows 8g + 4hi .. +3
+            if constexpr (DQ) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                u32x2 w = {T::pack2(ds[4 * g + 0], ds[4 * g + 1]), T::pack2(ds[4 * g + 2], ds[4 * g + 3])};
-                lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), w);
+                for (int g = 0; g < 4; ++g) {
+                    u32x2 w = {T::pack2(ds[4 * g + 0], ds[4 * g + 1]), T::pack2(ds[4 * g + 2], ds[4 * g + 3])};
+                    lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), w);
+                }
             }
-        } else {
+        } else if (DQ) {
             // keys of this wave are all above the causal diagonal for this query tile: dS = 0
             const u32x2 z = {0u, 0u};
 #pragma unroll
             for (int g = 0; g < 4; ++g) lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), z);
         }
-        __syncthreads();
+        if constexpr (DQ) {
+            __syncthreads();
 
-        // ---- dQ[q][d] += dS[q][key] K[key][d] over the BKV keys (16x16x32 MFMAs); the
-        // 2*(D/16) output tiles of 16 query rows x 16 columns are dealt round-robin to the waves,
-        // each summing over every key of the block, so one fp32 atomic per element per block.
-#pragma unroll
-        for (int t0 = 0; t0 < 2 * (D / 16); t0 += C::NW) {
-            const int t = t0 + wave;
-            if (t < 2 * (D / 16)) {
-                const int qh = t & 1;
-                const int dbase = 16 * (t >> 1);
-                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-                auto dq_operands = [&](int ks, u32x4 &av, u32x4 &bv) __attribute__((always_inline)) {
-                    const int r0 = 32 * ks + 8 * g4 + qq;
-                    u32x2 a0 = lds_read_tr(dsimg, ds_off(r0, 16 * qh + 4 * pp));
-                    u32x2 a1 = lds_read_tr(dsimg, ds_off(r0 + 4, 16 * qh + 4 * pp));
-                    av = u32x4{a0[0], a0[1], a1[0], a1[1]};
-                    u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
-                    u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
-                    bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
-                };
-                if constexpr (FA_BWD_DQ_PREFETCH) {
-                    // operands of key step ks+1 are read before the MFMA of step ks
-                    u32x4 av, bv, avn, bvn;
-                    dq_operands(0, av, bv);
-#pragma unroll
-                    for (int ks = 0; ks < C::BKV / 32; ++ks) {
-                        if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
-                        acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
-                        av = avn;
-                        bv = bvn;
+            // ---- dQ[q][d] += dS[q][key] K[key][d] over the BKV keys (16x16x32 MFMAs); the
+            // 2*(D/16) output tiles of 16 query rows x 16 columns are dealt round-robin to the waves,
+            // each summing over every key of the block, so one fp32 atomic per element per block.
+    #pragma unroll
+            for (int t0 = 0; t0 < 2 * (D / 16); t0 += C::NW) {
+                const int t = t0 + wave;
+                if (t < 2 * (D / 16)) {
+                    const int qh = t & 1;
+                    const int dbase = 16 * (t >> 1);
+                    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                    auto dq_operands = [&](int ks, u32x4 &av, u32x4 &bv) __attribute__((always_inline)) {
+                        const int r0 = 32 * ks + 8 * g4 + qq;
+                        u32x2 a0 = lds_read_tr(dsimg, ds_off(r0, 16 * qh + 4 * pp));
+                        u32x2 a1 = lds_read_tr(dsimg, ds_off(r0 + 4, 16 * qh + 4 * pp));
+                        av = u32x4{a0[0], a0[1], a1[0], a1[1]};
+                        u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
+                        u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
+                        bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
+                    };
+                    if constexpr (FA_BWD_DQ_PREFETCH) {
+                        // operands of key step ks+1 are read before the MFMA of step ks
+                        u32x4 av, bv, avn, bvn;
+                        dq_operands(0, av, bv);
+    #pragma unroll
+                        for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                            if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
+                            acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
+                            av = avn;
+                            bv = bvn;
+                        }
+                    } else {
+    #pragma unroll
+                        for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                            u32x4 av, bv;
+                            dq_operands(ks, av, bv);
+                            acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
+                        }
                     }
-                } else {
-#pragma unroll
-                    for (int ks = 0; ks < C::BKV / 32; ++ks) {
-                        u32x4 av, bv;
-                        dq_operands(ks, av, bv);
-                        acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
-                    }
-                }
-                const int d = dbase + (lane & 15);
-                if (FA_BWD_FULLTILE && q0 + C::BQ <= seqlen_q && head_dim == D) {
-                    // full tile (wave-uniform test): the four atomics without per-lane guards
-                    float *base = dqa + (int64_t)(q0 + 16 * qh + 4 * g4) * dqa_row + d;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) atomicAdd(base + i * dqa_row, acc[i]);
-                } else if (d < head_dim) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int q = q0 + 16 * qh + 4 * g4 + i;
-                        if (q < seqlen_q) atomicAdd(dqa + (int64_t)q * dqa_row + d, acc[i]);
+                    const int d = dbase + (lane & 15);
+                    if (FA_BWD_FULLTILE && q0 + C::BQ <= seqlen_q && head_dim == D) {
+                        // full tile (wave-uniform test): the four atomics without per-lane guards
+                        float *base = dqa + (int64_t)(q0 + 16 * qh + 4 * g4) * dqa_row + d;
+    #pragma unroll
+                        for (int i = 0; i < 4; ++i) atomicAdd(base + i * dqa_row, acc[i]);
+                    } else if (d < head_dim) {
+    #pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int q = q0 + 16 * qh + 4 * g4 + i;
+                            if (q < seqlen_q) atomicAdd(dqa + (int64_t)q * dqa_row + d, acc[i]);
+                        }
                     }
                 }
             }

@@ -74,7 +74,7 @@ template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE>
 static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     if constexpr (D == 128 && FA_BWD_SPLIT128) {
         // dQ either by the split kernel's atomics or by the query-major pass (bwd_dq_direct)
-        constexpr bool DQK = FA_BWD_DQK && !DROPOUT && !SPARSE;
+        constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
         using C = BwdSplitCfg<D, CAUSAL>;
         auto kern = fa_bwd_split_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
         static const hipError_t attr_err =
@@ -95,12 +95,23 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
         return hipGetLastError();
     }
     using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value, CAUSAL>;
-    auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT, SPARSE>;
+    constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
+    auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
     static const hipError_t attr_err =
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
     if (attr_err != hipSuccess) return attr_err;
     dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
     hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
+    if constexpr (DQK) {
+        constexpr int NWQ = 8;
+        using CQ = DqCfg<D, NWQ>;
+        auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
+        static const hipError_t attr_q =
+            hipFuncSetAttribute((const void *)kq, hipFuncAttributeMaxDynamicSharedMemorySize, CQ::LDS_BYTES);
+        if (attr_q != hipSuccess) return attr_q;
+        dim3 gq((a.max_seqlen_q + CQ::BM - 1) / CQ::BM, a.nheads, a.batch);
+        hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a);
+    }
     return hipGetLastError();
 }
 

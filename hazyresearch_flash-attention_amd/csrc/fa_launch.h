@@ -26,9 +26,13 @@ hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t stream);
 #define FA_BWD_DQK 1        // 1: D = 128 dense, no dropout: dQ by the query-major fa_bwd_dq_kernel
 #endif
 // true when launch_bwd writes dq itself (no fp32 accumulator, no convert pass)
+#ifndef FA_BWD_DQK_MIN_D
+#define FA_BWD_DQK_MIN_D 128   // smallest head-dim tile that takes the query-major dQ pass
+#endif
+constexpr bool bwd_dqk_tile(int D) { return FA_BWD_DQK && D >= FA_BWD_DQK_MIN_D && (D < 128 || FA_BWD_SPLIT128); }
 inline bool bwd_dq_direct(const FaBwdArgs &a, const FaBlockMask &bm) {
-    return FA_BWD_SPLIT128 && FA_BWD_DQK && a.head_dim > 64 && a.p_dropout == 0.f && bm.mask == nullptr &&
-           a.max_seqlen_k > 0;
+    const int tile = a.head_dim <= 32 ? 32 : a.head_dim <= 64 ? 64 : 128;
+    return bwd_dqk_tile(tile) && a.p_dropout == 0.f && bm.mask == nullptr && a.max_seqlen_k > 0;
 }
 hipError_t launch_bwd_post(const FaBwdArgs &a, hipStream_t stream);
 }  // namespace fa

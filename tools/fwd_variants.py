@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "nodqk": {"FA_BWD_DQK": 0},
+    "dqk64": {"FA_BWD_DQK_MIN_D": 32},
 }
 
 CONFIGS = [
@@ -152,6 +152,8 @@ BWD_CONFIGS = [
     # name, B, H, S, D, causal, p
     ("bwd_ns_B8_H12_S2048_D64", 8, 12, 2048, 64, False, 0.0),
     ("bwd_c3_B8_H12_S2048_D64_causal_p0.1", 8, 12, 2048, 64, True, 0.1),
+    ("bwd_c_B8_H12_S2048_D64_causal", 8, 12, 2048, 64, True, 0.0),
+    ("bwd_ns_B8_H12_S2048_D32", 8, 12, 2048, 32, False, 0.0),
     ("bwd_ns_B8_H12_S2048_D128", 8, 12, 2048, 128, False, 0.0),
     ("bwd_c_B8_H12_S2048_D128_causal", 8, 12, 2048, 128, True, 0.0),
 ]
