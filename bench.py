@@ -242,6 +242,21 @@ def main():
         fl = fwd_flops(8, 12, 2048, 2048, 64, True) * 3.5
         extra["c3_B8_H12_S2048_D64_bf16_causal_p0.1_fwd_bwd"] = {
             "ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2), "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
+        del q3, k3, v3, gout
+        # C4 forward + backward (D = 128, causal: the reference's d128 chart setting, README.md:92-99)
+        q4, k4, v4, _, c4q, c4k = make_inputs(16, 12, 4096, 4096, 128, torch.bfloat16, dev)
+        q4.requires_grad_(); k4.requires_grad_(); v4.requires_grad_()
+        gout4 = torch.randn_like(q4)
+
+        def fb4():
+            o = flash_attn_unpadded_func(q4, k4, v4, c4q, c4k, 4096, 4096, 0.0, causal=True)
+            torch.autograd.grad(o, (q4, k4, v4), gout4)
+
+        ms, _ = time_events(fb4, 5, 10)
+        fl = fwd_flops(16, 12, 4096, 4096, 128, True) * 3.5
+        extra["c4_B16_H12_S4096_D128_bf16_causal_fwd_bwd"] = {
+            "ms": round(ms, 4), "TFLOPS": round(fl / ms / 1e9, 2), "frac_peak": round(fl / ms / 1e9 / PEAK_BF16_TFLOPS, 4)}
+        del q4, k4, v4, gout4
 
     if not args.no_extra and rank == 0:
         # the reference's published metric (README.md:69-81): fwd+bwd speedup over PyTorch standard

@@ -26,8 +26,10 @@ def rows(pattern):
 def kind(name):
     if "fa_fwd_kernel" in name:
         return "fwd"
-    if "fa_bwd_kernel" in name:
+    if "fa_bwd_kernel" in name or "fa_bwd_split_kernel" in name:
         return "bwd_main"
+    if "fa_bwd_dq_kernel" in name:
+        return "bwd_dq"
     if "fa_bwd_dot_kernel" in name:
         return "bwd_delta"
     if "fa_bwd_dq_convert" in name:
@@ -50,9 +52,14 @@ for D in (32, 64, 128):
             if k:
                 pmc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     fwd_fl = 4.0 * B * H * S * S * D
+    # D = 128: the key-major kernel does S, dZ, dV, dK (2.0x forward FLOPs) and no dQ; the
+    # query-major dQ pass recomputes S and dP and does dQ (1.5x forward FLOPs), no atomics
+    split = D == 128
     alg = {
         "fwd": (fwd_fl, 2 * (2 * B * S * H * D) * 2 + 4 * B * H * S),
-        "bwd_main": (2.5 * fwd_fl, (5 * B * S * H * D) * 2 + 8 * B * H * S + 4 * B * S * H * D * (S // 256) * 2),
+        "bwd_main": ((2.0 if split else 2.5) * fwd_fl,
+                     (5 * B * S * H * D) * 2 + 8 * B * H * S + (0 if split else 4 * B * S * H * D * (S // 256) * 2)),
+        "bwd_dq": (1.5 * fwd_fl, (4 * B * S * H * D) * 2 + 8 * B * H * S),
         "bwd_delta": (0.0, 2 * B * S * H * D * 2 + 4 * B * H * S + 4 * B * S * H * D),
         "bwd_dq_convert": (0.0, 4 * B * S * H * D + 2 * B * S * H * D),
     }
@@ -75,7 +82,8 @@ for D in (32, 64, 128):
             e["mfma_busy"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc), 4)
         out[k] = e
     res[f"D{D}"] = {"config": f"B={B} H={H} S={S} D={D} bf16 non-causal", "kernels": out}
-res["notes"] = ("bwd_main algorithmic bytes count q,k,v,dO reads, dk/dv writes, lse/delta and the fp32 dQ "
-                "atomics (one partial per 256-key block); durations from rocprofv3 kernel trace; PMC passes "
+res["notes"] = ("bwd_main algorithmic bytes count q,k,v,dO reads, dk/dv writes, lse/delta and (D <= 64) the fp32 "
+                "dQ atomics (one partial per 256-key block); D = 128 runs the P/dS split kernel plus the query-major "
+                "dQ pass (bwd_dq: q,k,v,dO reads, dq write); durations from rocprofv3 kernel trace; PMC passes "
                 "run separately (profiled clocks read ~2-5 % low)")
 print(json.dumps(res, indent=1))
