@@ -252,6 +252,43 @@ def test_empty_and_ragged_sequences():
         assert err <= max_err_bound(pt, ref, floor=1e-2), (b, err)
 
 
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [64, 128])
+def test_empty_and_ragged_sequences_backward(d, causal):
+    """Backward on zero-length and 1-token sequences: zero dQ for empty key sets, zero dK/dV for
+    empty query sets, the 2x rule elsewhere. d=128 runs the P/dS split kernel plus the query-major
+    dQ pass (no dq workspace, no convert pass), d=64 the atomic-dQ kernel."""
+    fi = _fa()
+    H = 2
+    lens_q = [5, 0, 1, 130, 64, 3]
+    lens_k = [7, 3, 0, 129, 1, 300]
+    cu_q = torch.tensor([0] + list(np.cumsum(lens_q)), dtype=torch.int32, device=DEV)
+    cu_k = torch.tensor([0] + list(np.cumsum(lens_k)), dtype=torch.int32, device=DEV)
+    g = torch.Generator().manual_seed(1)
+    q = torch.randn(sum(lens_q), H, d, generator=g).bfloat16().to(DEV).requires_grad_()
+    k = torch.randn(sum(lens_k), H, d, generator=g).bfloat16().to(DEV).requires_grad_()
+    v = torch.randn(sum(lens_k), H, d, generator=g).bfloat16().to(DEV).requires_grad_()
+    out = fi.flash_attn_unpadded_func(q, k, v, cu_q, cu_k, max(lens_q), max(lens_k), 0.0, causal=causal)
+    gout = torch.randn(out.shape, generator=g).bfloat16().to(DEV)
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), gout)
+    for b in range(len(lens_q)):
+        qs, ks = slice(int(cu_q[b]), int(cu_q[b + 1])), slice(int(cu_k[b]), int(cu_k[b + 1]))
+        if lens_q[b] == 0:
+            assert (dk[ks] == 0).all() and (dv[ks] == 0).all()
+            continue
+        if lens_k[b] == 0:
+            assert (dq[qs] == 0).all()
+            continue
+        qb, kb, vb = [t.detach()[sl][None].requires_grad_() for t, sl in ((q, qs), (k, ks), (v, ks))]
+        ref, _ = attention_ref(qb, kb, vb, causal=causal)
+        pt, _ = attention_ref(qb, kb, vb, causal=causal, upcast=False, reorder_ops=True)
+        refs = torch.autograd.grad(ref, (qb, kb, vb), gout[qs][None])
+        pts = torch.autograd.grad(pt, (qb, kb, vb), gout[qs][None])
+        for name, a, r, lo in zip(("dq", "dk", "dv"), (dq[qs], dk[ks], dv[ks]), refs, pts):
+            err = (a.float() - r[0].float()).abs().max().item()
+            assert err <= max_err_bound(lo, r, floor=1e-2), (b, name, err)
+
+
 def test_invalid_arguments_raise():
     fi = _fa()
     q = torch.randn(16, 2, 60, device=DEV, dtype=torch.float16)

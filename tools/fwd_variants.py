@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "dqk64": {"FA_BWD_DQK_MIN_D": 32},
+    "q0": {"FA_BWD_QPF2": 0},
 }
 
 CONFIGS = [
