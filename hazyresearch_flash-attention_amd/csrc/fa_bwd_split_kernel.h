@@ -18,6 +18,13 @@
 
 namespace fa {
 
+#ifndef FA_BWD_SPLIT_KVL
+#define FA_BWD_SPLIT_KVL 1   // 1: split kernels re-read K / V rows from LDS (no 32-register copy)
+#endif
+#ifndef FA_BWD_SPLIT_KVL_NC
+#define FA_BWD_SPLIT_KVL_NC 1   // 1: the non-causal ones too (D=128 non-causal 1.00 -> 0.95 ms)
+#endif
+
 template <int D, bool KVL_ = false>
 struct BwdSplitCfg {
     static constexpr int NW = 8;            // waves per workgroup
@@ -50,7 +57,7 @@ struct BwdSplitCfg {
 // DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
 __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a, const FaBlockMask bm) {
-    using C = BwdSplitCfg<D, CAUSAL>;
+    using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];

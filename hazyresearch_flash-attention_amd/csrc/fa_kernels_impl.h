@@ -75,7 +75,7 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
     if constexpr (D == 128 && FA_BWD_SPLIT128) {
         // dQ either by the split kernel's atomics or by the query-major pass (bwd_dq_direct)
         constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
-        using C = BwdSplitCfg<D, CAUSAL>;
+        using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL>;
         auto kern = fa_bwd_split_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
         static const hipError_t attr_err =
             hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);

@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "q0": {"FA_BWD_QPF2": 0},
+    "kvreg": {"FA_BWD_SPLIT_KVL": 0},
 }
 
 CONFIGS = [
