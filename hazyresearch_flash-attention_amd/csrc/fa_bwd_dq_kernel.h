@@ -19,6 +19,10 @@
 
 namespace fa {
 
+#ifndef FA_BWD_DQ_XCD
+#define FA_BWD_DQ_XCD 1   // 1: XCD-aware block order (non-causal)
+#endif
+
 template <int D, int NW>
 struct DqCfg {
     static constexpr int BM = 32 * NW;    // query rows per workgroup
@@ -41,8 +45,22 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a
     const int nqb = gridDim.x;
     const int nbh = gridDim.y * gridDim.z;
     const int L = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
-    const int qb = CAUSAL ? nqb - 1 - L / nbh : (int)blockIdx.x;
-    const int bh_lin = CAUSAL ? L % nbh : (int)(blockIdx.y + gridDim.y * blockIdx.z);
+    int qb, bh_lin;
+    if (CAUSAL) {
+        qb = nqb - 1 - L / nbh;
+        bh_lin = L % nbh;
+    } else if (FA_BWD_DQ_XCD) {
+        // XCD-aware (as the forward): blocks L and L+8 share an XCD; each XCD gets a contiguous
+        // run of (head, q-block), so a head's K/V stream through one L2 (bijective for any count)
+        const int nwg = nqb * nbh;
+        const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
+        const int Lp = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+        qb = Lp % nqb;
+        bh_lin = Lp / nqb;
+    } else {
+        qb = blockIdx.x;
+        bh_lin = blockIdx.y + gridDim.y * blockIdx.z;
+    }
     const int h = bh_lin % a.nheads;
     const int b = bh_lin / a.nheads;
 

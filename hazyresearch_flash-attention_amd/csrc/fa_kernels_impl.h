@@ -7,6 +7,10 @@
 #include "fa_bwd_split_kernel.h"
 #include "fa_bwd_dq_kernel.h"
 
+#ifndef FA_BWD_DQ_NW
+#define FA_BWD_DQ_NW 8   // waves (32 query rows each) per dQ-pass workgroup
+#endif
+
 #include <cstdlib>
 
 namespace fa {
@@ -83,7 +87,7 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
         dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
         hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
         if constexpr (DQK) {
-            constexpr int NWQ = 8;
+            constexpr int NWQ = FA_BWD_DQ_NW;
             using CQ = DqCfg<D, NWQ>;
             auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
             static const hipError_t attr_q =
@@ -103,7 +107,7 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
     dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
     hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
     if constexpr (DQK) {
-        constexpr int NWQ = 8;
+        constexpr int NWQ = FA_BWD_DQ_NW;
         using CQ = DqCfg<D, NWQ>;
         auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
         static const hipError_t attr_q =
