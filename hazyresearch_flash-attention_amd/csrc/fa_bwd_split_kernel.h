@@ -75,6 +75,17 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
         kb = L / nbh;
         h = (L % nbh) % gridDim.y;
         b = (L % nbh) / gridDim.y;
+    } else if (FA_BWD_XCD) {
+        // XCD-aware: blocks L and L+8 share an XCD; each XCD gets a contiguous run of (head, key
+        // block), so the key blocks of one head stream its Q/dO tiles through one L2 together
+        const int nkb = gridDim.x;
+        const int nwg = nkb * gridDim.y * gridDim.z;
+        const int L = blockIdx.x + nkb * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
+        const int Lp = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+        kb = Lp % nkb;
+        h = (Lp / nkb) % gridDim.y;
+        b = (Lp / nkb) / gridDim.y;
     }
     const int q_start = a.cu_seqlens_q[b];
     const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;

@@ -22,7 +22,7 @@ BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
     "base": {},
-    "noxcd": {"FA_BWD_DQ_XCD": 0},
+    "noxcd": {"FA_BWD_XCD": 0},
 }
 
 CONFIGS = [
