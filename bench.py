@@ -29,6 +29,7 @@ import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 flop/clk x 2.4 GHz, dense (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+CLOCK_WARMUP_S = 0.25   # untimed, time-based warm-up before every timed region
 
 
 def fwd_flops(B, H, Sq, Sk, D, causal):
@@ -55,12 +56,17 @@ def make_inputs(B, H, Sq, Sk, D, dtype, dev, kvpacked=False, seed=0):
     return q, k, v, kv, cu_q, cu_k
 
 
-def time_events(fn, iters, warmup, reps=5):
+def time_events(fn, iters, warmup, reps=5, min_warm_s=0.05):
     """Average device time per call of fn(): HIP events on torch's current stream (where the
-    library launches) around `iters` back-to-back calls, median of `reps` batches."""
+    library launches) around `iters` back-to-back calls, median of `reps` batches, after
+    `warmup` calls and at least `min_warm_s` of further untimed calls (clock ramp)."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < min_warm_s:
+        fn()
+        torch.cuda.synchronize()
     per = []
     for _ in range(reps):
         s = torch.cuda.Event(enable_timing=True)
@@ -142,6 +148,17 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # The GPU clock ramps over the first ~30 ms of load: whatever --warmup says,
+    # keep launching untimed steps until CLOCK_WARMUP_S of device time has passed, so the timed
+    # region measures the steady state.
+    t_w = time.perf_counter()
+    n_clock = 0
+    while time.perf_counter() - t_w < CLOCK_WARMUP_S:
+        for _ in range(20):
+            step()
+        n_clock += 20
+        torch.cuda.synchronize()
+    clock_warm_ms = (time.perf_counter() - t_w) * 1e3
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -292,6 +309,8 @@ def main():
                        "global_batch": B * world, "seq_len": S, "heads": H, "head_dim": D,
                        "parallelism": f"replicas x{world} (no collective)"},
             "frac_peak": round(value / world / PEAK_BF16_TFLOPS, 4),
+            "clock_warmup": {"ms": round(clock_warm_ms, 1), "steps": n_clock,
+                             "note": "untimed steps after --warmup, always run (time-based)"},
             "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
         }
         print(json.dumps(line), flush=True)

@@ -83,6 +83,15 @@ int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {
         case FA_QUERY_MASK_ARGS_SIZE: return (int64_t)sizeof(FaBlockMask);
         case FA_QUERY_PAD_WORKSPACE: return a * (int64_t)sizeof(int32_t);
         case FA_QUERY_ROTARY_ARGS_SIZE: return (int64_t)sizeof(FaRotaryArgs);
+        case FA_QUERY_BWD_WORKSPACE_NEEDED: {
+            // a = head_dim, b = p_dropout > 0, c = block-sparse: 1 if fa_bwd needs dq_accum
+            FaBwdArgs t{};
+            t.head_dim = (int32_t)a;
+            t.p_dropout = b ? 0.5f : 0.f;
+            t.max_seqlen_k = 1;
+            const FaBlockMask m = {c ? (const uint8_t *)1 : nullptr, 0, 0, 0};
+            return fa::bwd_dq_direct(t, m) ? 0 : 1;
+        }
         default: return -1;
     }
 }
@@ -115,6 +124,9 @@ int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
         (a->q_row_stride | a->k_row_stride | a->v_row_stride | a->o_row_stride | a->q_head_stride |
          a->k_head_stride | a->v_head_stride | a->o_head_stride) % 8 != 0)
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: q/k/v/o must be 16-byte aligned with strides multiple of 8");
+    if (a->q_row_stride < a->head_dim || a->k_row_stride < a->head_dim || a->v_row_stride < a->head_dim ||
+        a->o_row_stride < a->head_dim)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: row strides must be >= head_dim (no overlapping/broadcast rows)");
     if (a->s_dmask && (a->s_rows < a->max_seqlen_q || a->s_cols < a->max_seqlen_k))
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: s_dmask extents smaller than max_seqlen");
     // the forward addresses each sequence through 32-bit buffer offsets
@@ -141,16 +153,34 @@ int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
 int bwd_impl(const FaBwdArgs *a, const FaBlockMask &bm, void *stream) {
     int rc = check_common(a, "fa_bwd");
     if (rc) return rc;
-    if (!a->dout || !a->out || !a->dq || !a->dk || !a->dv || !a->softmax_d || !a->dq_accum)
+    if (!a->dout || !a->out || !a->dq || !a->dk || !a->dv || !a->softmax_d)
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: NULL tensor pointer");
+    // the fp32 dQ workspace is only touched when dq is not written directly
+    const bool direct = fa::bwd_dq_direct(*a, bm);
+    if (!direct && !a->dq_accum)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: dq_accum is NULL (required unless fa_query(FA_QUERY_BWD_WORKSPACE_NEEDED) is 0)");
     if (!aligned16(a->q) || !aligned16(a->k) || !aligned16(a->v) || !aligned16(a->dout) || !aligned16(a->out) ||
-        !aligned16(a->dq) || !aligned16(a->dk) || !aligned16(a->dv) || !aligned16(a->dq_accum) ||
+        !aligned16(a->dq) || !aligned16(a->dk) || !aligned16(a->dv) || (a->dq_accum && !aligned16(a->dq_accum)) ||
         (a->q_row_stride | a->k_row_stride | a->v_row_stride | a->o_row_stride | a->do_row_stride |
          a->dq_row_stride | a->dk_row_stride | a->dv_row_stride | a->q_head_stride | a->k_head_stride |
          a->v_head_stride | a->o_head_stride | a->do_head_stride | a->dq_head_stride | a->dk_head_stride |
          a->dv_head_stride) % 8 != 0)
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: tensors must be 16-byte aligned with strides multiple of 8");
     if (a->total_q < 0) return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: total_q < 0");
+    if (a->q_row_stride < a->head_dim || a->k_row_stride < a->head_dim || a->v_row_stride < a->head_dim ||
+        a->o_row_stride < a->head_dim || a->do_row_stride < a->head_dim || a->dq_row_stride < a->head_dim ||
+        a->dk_row_stride < a->head_dim || a->dv_row_stride < a->head_dim)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: row strides must be >= head_dim (no overlapping/broadcast rows)");
+    // the backward kernels address each sequence through 32-bit buffer offsets, like the forward
+    const int64_t lim = (int64_t)1 << 31;
+    const int64_t q_span = (int64_t)a->max_seqlen_q * 2, k_span = (int64_t)a->max_seqlen_k * 2;   // bytes per unit stride
+    if (q_span * a->q_row_stride >= lim || q_span * a->do_row_stride >= lim ||
+        q_span * a->dq_row_stride >= lim || q_span * a->o_row_stride >= lim ||
+        k_span * a->k_row_stride >= lim || k_span * a->v_row_stride >= lim ||
+        k_span * a->dk_row_stride >= lim || k_span * a->dv_row_stride >= lim)
+        return fail(FA_ERR_UNSUPPORTED, "fa_bwd: a sequence spans more than 2 GiB (seqlen * row_stride)");
+    // nothing to do without query rows: dq/dk/dv are the caller's (zero_tensors), softmax_d unused
+    if (a->max_seqlen_q == 0) return FA_OK;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = fa::launch_bwd_pre(*a, s);
     if (e != hipSuccess) return hip_fail(e, "fa_bwd pre launch");
@@ -162,7 +192,7 @@ int bwd_impl(const FaBwdArgs *a, const FaBlockMask &bm, void *stream) {
         }
         if (e != hipSuccess) return hip_fail(e, "fa_bwd launch");
     }
-    if (!fa::bwd_dq_direct(*a, bm)) {
+    if (!direct) {
         e = fa::launch_bwd_post(*a, s);
         if (e != hipSuccess) return hip_fail(e, "fa_bwd post launch");
     }

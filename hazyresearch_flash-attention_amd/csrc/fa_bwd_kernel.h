@@ -43,12 +43,6 @@ namespace fa {
 #ifndef FA_BWD_DQ_PREFETCH
 #define FA_BWD_DQ_PREFETCH 1    // 1: dQ MFMA operands read one key step ahead
 #endif
-#ifndef FA_BWD_XCD
-#define FA_BWD_XCD 0            // 1: XCD-aware block order in the non-causal key-major kernels (A/B: -10 % at D=64: the dQ atomics of one head collide)
-#endif
-#ifndef FA_BWD_KV_LDS8
-#define FA_BWD_KV_LDS8 0        // 1: the same for the non-causal kernels (A/B: 2-5 % slower there)
-#endif
 
 // Waves per workgroup (32 keys each). dQ atomic bytes scale with 1/NW, so both use 8 at D <= 64
 // (causal: 4-wave blocks balanced the triangle better but were slower once K/V moved to LDS).
@@ -80,7 +74,7 @@ struct BwdCfg {
     // instead of being held in 32 registers for the whole kernel. The causal kernels (mask and
     // LPT bookkeeping on top) spilled inside the loop without it (C3 backward 0.557 -> 0.398 ms
     // on 4-wave blocks); the non-causal ones fit and lose 2-5 % with it.
-    static constexpr bool KV_LDS = FA_BWD_KV_LDS && D <= 64 && (CAUSAL_ || FA_BWD_KV_LDS8);
+    static constexpr bool KV_LDS = FA_BWD_KV_LDS && D <= 64 && CAUSAL_;
     static constexpr int OFF_V = OFF_QLIVE + QLIVE_WORDS * 8;
     static constexpr int LDS_BYTES = OFF_V + (KV_LDS ? K_IMG : 0);
     static constexpr int QCH = (BQ * NC + NT - 1) / NT;   // staged 16-B chunks per thread per tile
@@ -92,7 +86,7 @@ struct BwdCfg {
 // apart per half-wave) touch every bank once.
 __device__ __forceinline__ int ds_off(int r, int q) { return r * 64 + ((q * 2) ^ (((r >> 1) & 7) << 3)); }
 
-// delta = rowsum(dO * O) (softmax_d), and zero the fp32 dQ accumulator. 16 threads per row
+// delta = rowsum(dO * O) (softmax_d), and zero the fp32 dQ accumulator (if any). 16 threads per row
 // (one 16-B chunk each), 16 rows per 256-thread block, shuffle reduction over the 16 lanes.
 template <typename T>
 __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const FaBwdArgs a) {
@@ -114,10 +108,12 @@ __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const FaBwdArgs a) {
             sum += T::to_float(x[e] & 0xFFFF) * T::to_float(y[e] & 0xFFFF);
             sum += T::to_float(x[e] >> 16) * T::to_float(y[e] >> 16);
         }
-        float *acc = a.dq_accum + ((int64_t)(q_start + row) * a.nheads + h) * a.head_dim + c * 8;
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<f32x4 *>(acc) = z;
-        *reinterpret_cast<f32x4 *>(acc + 4) = z;
+        if (a.dq_accum) {   // NULL when dq is written directly (bwd_dq_direct)
+            float *acc = a.dq_accum + ((int64_t)(q_start + row) * a.nheads + h) * a.head_dim + c * 8;
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<f32x4 *>(acc) = z;
+            *reinterpret_cast<f32x4 *>(acc + 4) = z;
+        }
     }
 #pragma unroll
     for (int w = 8; w >= 1; w >>= 1) sum += __shfl_xor(sum, w, 16);
@@ -176,17 +172,6 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         kb = L / nbh;
         h = (L % nbh) % gridDim.y;
         b = (L % nbh) / gridDim.y;
-    } else if (FA_BWD_XCD) {
-        // XCD-aware: blocks L and L+8 share an XCD; each XCD gets a contiguous run of (head, key
-        // block), so the key blocks of one head stream its Q/dO tiles through one L2 together
-        const int nkb = gridDim.x;
-        const int nwg = nkb * gridDim.y * gridDim.z;
-        const int L = blockIdx.x + nkb * (blockIdx.y + gridDim.y * blockIdx.z);
-        const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
-        const int Lp = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
-        kb = Lp % nkb;
-        h = (Lp / nkb) % gridDim.y;
-        b = (Lp / nkb) / gridDim.y;
     }
     const int q_start = a.cu_seqlens_q[b];
     const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
@@ -250,7 +235,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     const float rp = 1.0f / (1.0f - a.p_dropout);
     const uint32_t keep_thr = (uint32_t)floorf((1.0f - a.p_dropout) * 65535.0f);
     const uint32_t seed_lo = (uint32_t)a.rng_seed, seed_hi = (uint32_t)(a.rng_seed >> 32);
-    const uint32_t rng_ctr3 = (uint32_t)(a.rng_offset >> 2);
+    const uint32_t rng_ctr3 = DROPOUT ? (uint32_t)(rng_offset_of(a) >> 2) : 0u;
     const uint32_t bh = (uint32_t)(b * a.nheads + h);
 
     const int grp = (lane >> 4) & 1;   // 16-lane group within the half (32x32 tr reads)
@@ -623,7 +608,7 @@ __global__ __launch_bounds__(256) void fa_probs_kernel(const FaFwdArgs a, const 
         u32x4 w = {0u, 0u, 0u, 0u};
         if (DROPOUT) {
             const uint32_t g = ((uint32_t)(q0 >> 5) << 2) | (sg << 1) | hh;
-            w = philox7(g, (uint32_t)col, bh, (uint32_t)(a.rng_offset >> 2), (uint32_t)a.rng_seed,
+            w = philox7(g, (uint32_t)col, bh, (uint32_t)(rng_offset_of(a) >> 2), (uint32_t)a.rng_seed,
                         (uint32_t)(a.rng_seed >> 32));
         }
         for (int slot = 0; slot < 8; ++slot) {

@@ -75,17 +75,6 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
         kb = L / nbh;
         h = (L % nbh) % gridDim.y;
         b = (L % nbh) / gridDim.y;
-    } else if (FA_BWD_XCD) {
-        // XCD-aware: blocks L and L+8 share an XCD; each XCD gets a contiguous run of (head, key
-        // block), so the key blocks of one head stream its Q/dO tiles through one L2 together
-        const int nkb = gridDim.x;
-        const int nwg = nkb * gridDim.y * gridDim.z;
-        const int L = blockIdx.x + nkb * (blockIdx.y + gridDim.y * blockIdx.z);
-        const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
-        const int Lp = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
-        kb = Lp % nkb;
-        h = (Lp / nkb) % gridDim.y;
-        b = (Lp / nkb) / gridDim.y;
     }
     const int q_start = a.cu_seqlens_q[b];
     const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
@@ -149,7 +138,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
     const float rp = 1.0f / (1.0f - a.p_dropout);
     const uint32_t keep_thr = (uint32_t)floorf((1.0f - a.p_dropout) * 65535.0f);
     const uint32_t seed_lo = (uint32_t)a.rng_seed, seed_hi = (uint32_t)(a.rng_seed >> 32);
-    const uint32_t rng_ctr3 = (uint32_t)(a.rng_offset >> 2);
+    const uint32_t rng_ctr3 = DROPOUT ? (uint32_t)(rng_offset_of(a) >> 2) : 0u;
     const uint32_t bh = (uint32_t)(b * a.nheads + h);
 
     const int grp = (lane >> 4) & 1;

@@ -205,6 +205,13 @@ __device__ __forceinline__ u32x4 philox7(uint32_t c0, uint32_t c1, uint32_t c2, 
     return r;
 }
 
+// Philox stream offset of a launch: the host-reserved rng_offset plus, when given, a device word
+// that a captured graph advances on every replay (FaFwdArgs::rng_offset_dev).
+template <typename A>
+__device__ __forceinline__ uint64_t rng_offset_of(const A &a) {
+    return a.rng_offset + (a.rng_offset_dev ? *a.rng_offset_dev : 0ull);
+}
+
 __device__ __forceinline__ uint32_t rng_group(int row) {
     return ((uint32_t)(row >> 5) << 2) | (((row >> 4) & 1) << 1) | ((row >> 2) & 1);
 }

@@ -30,48 +30,13 @@
 
 namespace fa {
 
-// Structure switches (compile-time; tools/fwd_variants.py builds and A/B-times combinations).
-#ifndef FA_FWD_PIPE
-#define FA_FWD_PIPE 0      // 1: software-pipeline QK^T of tile j+1 under the softmax of tile j (T15)
-#endif
-#ifndef FA_FWD_SCHED
-#define FA_FWD_SCHED 0     // 1: pin the MFMA/VALU interleave with sched_group_barrier (T19)
-#endif
-#ifndef FA_FWD_MFMA_SUM
-#define FA_FWD_MFMA_SUM 0  // 1: row sums of P by an MFMA with a constant all-ones A operand
-#endif
-#ifndef FA_FWD_PKFMA
-#define FA_FWD_PKFMA 0     // 1: exponent arguments with v_pk_fma_f32 (two per instruction)
-#endif
-#ifndef FA_FWD_SETPRIO
-#define FA_FWD_SETPRIO 0   // 1: static s_setprio 1 for the second half of the waves (T5 static form)
-#endif
-#ifndef FA_FWD_PINGPONG
-#define FA_FWD_PINGPONG 0  // 1: two half-workgroups half a tile apart (matrix/VALU phases paired)
-#endif
-#ifndef FA_FWD_WIDE_STORE
-#define FA_FWD_WIDE_STORE 1  // epilogue: 16-byte O stores via v_permlane32_swap (0: 8-byte stores)
-#endif
+// Register budget of the block-sparse kernels without dropout (waves per SIMD).
 #ifndef FA_FWD_SPARSE_WPE
-#define FA_FWD_SPARSE_WPE 4   // block-sparse kernels without dropout: register budget for 4 waves/SIMD
+#define FA_FWD_SPARSE_WPE 4
 #endif
-#ifndef FA_FWD_SOFF
-#define FA_FWD_SOFF 1      // 1: K/V tile loads = lane-constant offset + scalar tile offset; rows past the
-#endif                     //    end are cut by the buffer's record count (no per-tile vector bounds math)
-#ifndef FA_FWD_MTHR
-#define FA_FWD_MTHR 1      // 1: rescale test = one compare against a per-row threshold kept as state
-#endif
-#ifndef FA_FWD_DMA
-#define FA_FWD_DMA 1       // 1: dense K/V tiles staged by LDS-DMA (buffer_load ... lds, swizzle on the
-#endif                     //    source address) instead of registers + ds_write
+// 8-wave dense D<=64 kernels without dropout: minimum waves per SIMD (2 workgroups per CU).
 #ifndef FA_FWD_DENSE_WPE
-#define FA_FWD_DENSE_WPE 4   // 8-wave dense D<=64 kernels without dropout: minimum waves per SIMD (2 workgroups per CU)
-#endif
-#ifndef FA_FWD_LDS_PAD
-#define FA_FWD_LDS_PAD 0   // extra LDS bytes per workgroup (caps workgroups per CU; experiments)
-#endif
-#ifndef FA_FWD_WPS
-#define FA_FWD_WPS 0       // >0: __launch_bounds__ minimum waves per SIMD
+#define FA_FWD_DENSE_WPE 4
 #endif
 
 // NW = waves per workgroup (32 query rows each); chosen per launch (fa_kernels_impl.h).
@@ -86,7 +51,7 @@ struct FwdCfg {
     static constexpr int CPT = (BN * NC + NT - 1) / NT;   // staged chunks per thread per tile
     static constexpr int RNG_BYTES_PER_WAVE = 2 * 32 * 32 * 2;  // two 32x32 u16 images
     static constexpr int lds_bytes(bool dropout) {
-        return 4 * TILE_BYTES + (dropout ? NW * RNG_BYTES_PER_WAVE : 0) + FA_FWD_LDS_PAD;
+        return 4 * TILE_BYTES + (dropout ? NW * RNG_BYTES_PER_WAVE : 0);
     }
 };
 
@@ -140,11 +105,7 @@ constexpr int fwd_waves_per_eu(int D, int NW, bool dropout, bool sparse) {
                               : 1;
 }
 
-#if FA_FWD_WPS > 0
-#define FA_FWD_BOUNDS(NW) __launch_bounds__(64 * NW, FA_FWD_WPS)
-#else
 #define FA_FWD_BOUNDS(NW) __launch_bounds__(64 * NW)
-#endif
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
 __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu(D, NW, DROPOUT, SPARSE)))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
@@ -152,7 +113,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     constexpr float LN2 = 0.6931471805599453f;
-    constexpr bool MTHR = FA_FWD_MTHR && !SPARSE;   // measured slower on the block-sparse walk
+    constexpr bool MTHR = !SPARSE;   // one-compare rescale test; measured slower on the block-sparse walk
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     // ---- block -> (q-block, head, batch)
@@ -188,7 +149,6 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31;
     const int hi = lane >> 5;
-    if (FA_FWD_SETPRIO && wave >= C::NW / 2) __builtin_amdgcn_s_setprio(1);
     const int qw = q0 + 32 * wave;       // first query row of this wave
     const int qrow = qw + l32;           // the query row this lane owns
     const int head_dim = a.head_dim;
@@ -198,11 +158,11 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
     if (CAUSAL) n_end = min(n_end, q0 + C::BM);
     const int nt = (n_end + C::BN - 1) / C::BN;
 
-    // SOFF: the K/V descriptors end at row n_end, so rows past it read as zeros by themselves
+    // the K/V descriptors end at row n_end, so rows past it read as zeros by themselves
     const uint16_t *kbase = (const uint16_t *)a.k + (int64_t)k_start * a.k_row_stride + (int64_t)h * a.k_head_stride;
     const uint16_t *vbase = (const uint16_t *)a.v + (int64_t)k_start * a.v_row_stride + (int64_t)h * a.v_head_stride;
-    const auto kr = FA_FWD_SOFF ? make_rsrc_n(kbase, n_end * (int)a.k_row_stride * 2) : make_rsrc(kbase);
-    const auto vr = FA_FWD_SOFF ? make_rsrc_n(vbase, n_end * (int)a.v_row_stride * 2) : make_rsrc(vbase);
+    const auto kr = make_rsrc_n(kbase, n_end * (int)a.k_row_stride * 2);
+    const auto vr = make_rsrc_n(vbase, n_end * (int)a.v_row_stride * 2);
 
     // ---- block sparsity (fa_fwd_block): this lane's live 256-key column blocks, and their union
     // over the workgroup's rows, which drives the tile walk (dead columns are never loaded)
@@ -255,18 +215,17 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
         qf[ks] = as_frag<T>(w);
     }
 
-    // ---- register staging of K/V tiles (issue early, write late: T14). Loads are bounds-checked
-    // buffer loads: a tile past the end reads as zeros, so no branch is needed around them.
-    int st_off_k[C::CPT], st_off_v[C::CPT], st_lds[C::CPT], st_row[C::CPT], st_okc[C::CPT];
+    // ---- register staging of K/V tiles for the block-sparse walk (issue early, write late: T14).
+    // Loads are bounds-checked buffer loads: a tile past the end reads as zeros, so no branch is
+    // needed around them.
+    int st_off_k[C::CPT], st_off_v[C::CPT], st_lds[C::CPT];
 #pragma unroll
     for (int i = 0; i < C::CPT; ++i) {
         const int idx = tid + C::NT * i;
         const int row = idx / C::NC, c = idx % C::NC;
-        st_row[i] = idx < C::BN * C::NC ? row : (1 << 20);   // surplus threads load nothing
-        st_okc[i] = c * 8 < head_dim;
         st_off_k[i] = (row * (int)a.k_row_stride + c * 8) * 2;
         st_off_v[i] = (row * (int)a.v_row_stride + c * 8) * 2;
-        if (FA_FWD_SOFF && !(st_okc[i] && idx < C::BN * C::NC)) st_off_k[i] = st_off_v[i] = OOB;
+        if (!(c * 8 < head_dim && idx < C::BN * C::NC)) st_off_k[i] = st_off_v[i] = OOB;   // surplus threads load nothing
         st_lds[i] = S::off(row, c);
     }
     const int k_tile_step = C::BN * (int)a.k_row_stride * 2;
@@ -274,25 +233,11 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
     u32x4 kst[C::CPT], vst[C::CPT];
     auto gload_k = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < C::CPT; ++i) {
-            if (FA_FWD_SOFF) {
-                kst[i] = bload128s(kr, st_off_k[i], j * k_tile_step);
-            } else {
-                const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
-                kst[i] = bload128(kr, ok ? st_off_k[i] + j * k_tile_step : OOB);
-            }
-        }
+        for (int i = 0; i < C::CPT; ++i) kst[i] = bload128s(kr, st_off_k[i], j * k_tile_step);
     };
     auto gload_v = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < C::CPT; ++i) {
-            if (FA_FWD_SOFF) {
-                vst[i] = bload128s(vr, st_off_v[i], j * v_tile_step);
-            } else {
-                const bool ok = st_okc[i] && (j * C::BN + st_row[i] < n_end);
-                vst[i] = bload128(vr, ok ? st_off_v[i] + j * v_tile_step : OOB);
-            }
-        }
+        for (int i = 0; i < C::CPT; ++i) vst[i] = bload128s(vr, st_off_v[i], j * v_tile_step);
     };
     auto lds_store_k = [&](char *kb) __attribute__((always_inline)) {
 #pragma unroll
@@ -312,9 +257,6 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
         for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
     float m_i = -INFINITY;
     float l_i = 0.f;
-    f32x16 lsum;   // FA_FWD_MFMA_SUM: every register holds the running row sum of this lane's query
-#pragma unroll
-    for (int r = 0; r < 16; ++r) lsum[r] = 0.f;
     const float c_log2 = a.softmax_scale * LOG2E;
     const float thr_raw = RESCALE_THR / c_log2;
     float m_thr = -INFINITY;   // MTHR: rescale when a tile max passes this (m + thr_raw)
@@ -323,7 +265,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
     // dropout constants
     const uint32_t keep_thr = (uint32_t)floorf((1.0f - a.p_dropout) * 65535.0f);
     const uint32_t seed_lo = (uint32_t)a.rng_seed, seed_hi = (uint32_t)(a.rng_seed >> 32);
-    const uint32_t rng_ctr3 = (uint32_t)(a.rng_offset >> 2);
+    const uint32_t rng_ctr3 = DROPOUT ? (uint32_t)(rng_offset_of(a) >> 2) : 0u;
     const uint32_t bh = (uint32_t)(b * a.nheads + h);
     char *rng_img = smem + 4 * C::TILE_BYTES + wave * C::RNG_BYTES_PER_WAVE;
 
@@ -437,9 +379,6 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
                     mc_row = mcx;
                 }
                 l_i *= alpha;
-                if (FA_FWD_MFMA_SUM)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
 #pragma unroll
                 for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -453,9 +392,6 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
                 const float alpha = grow ? fast_exp2((m_i - m_new) * c_log2) : 1.f;
                 if (grow) m_i = m_new;
                 l_i *= alpha;
-                if (FA_FWD_MFMA_SUM)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
 #pragma unroll
                 for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -463,40 +399,17 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
             }
             mc = (m_i == -INFINITY ? 0.f : m_i) * c_log2;
         }
-        if (FA_FWD_PKFMA) {
-            typedef float f32x2 __attribute__((ext_vector_type(2)));
-            const f32x2 cc = {c_log2, c_log2}, mm = {-mc, -mc};
 #pragma unroll
-            for (int st = 0; st < 2; ++st)
+        for (int st = 0; st < 2; ++st)
 #pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                    f32x2 x = {s[st][r], s[st][r + 1]};
-                    x = __builtin_elementwise_fma(x, cc, mm);
-                    s[st][r] = fast_exp2(x[0]);
-                    s[st][r + 1] = fast_exp2(x[1]);
-                }
-        } else {
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
-        }
-        if (!FA_FWD_MFMA_SUM) l_i += sum_tree32(s[0], s[1]);
+            for (int r = 0; r < 16; ++r) s[st][r] = fast_exp2(fmaf(s[st][r], c_log2, -mc));
+        l_i += sum_tree32(s[0], s[1]);
 
         dropout_cvt(s, kv0, pf);
     };
 
-    // ---- O^T += V^T P^T for one tile (and the optional all-ones row-sum MFMA)
+    // ---- O^T += V^T P^T for one tile
     auto pv = [&](const char *vb, typename T::frag (&pf)[2][2]) __attribute__((always_inline)) {
-        if (FA_FWD_MFMA_SUM) {
-            const u32x4 ones = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};  // bf16 1.0
-            const u32x4 onesh = {0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u}; // fp16 1.0
-            const u32x4 one4 = std::is_same<T, Bf16>::value ? ones : onesh;
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) lsum = T::mfma32(as_frag<T>(one4), pf[st][s2], lsum);
-        }
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -510,48 +423,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
                 }
     };
 
-#if FA_FWD_PINGPONG
-    // ---- Ping-pong (two barriers per tile). Waves 0..NW/2-1 ("A") and NW/2..NW-1 ("B") share
-    // every SIMD pairwise and run half a tile apart, so each phase pairs one wave's matrix work
-    // with its partner's softmax:
-    //   iteration j, phase 1:  A: P·V(j-1), S(j) = K(j)Q^T   |  B: softmax(j-1)
-    //   iteration j, phase 2:  A: softmax(j)                  |  B: P·V(j-1), S(j)
-    // LDS: iteration j reads K(j) from kbuf[j&1] and V(j-1) from vbuf[(j-1)&1], and stages
-    // K(j+1) -> kbuf[(j+1)&1], V(j) -> vbuf[j&1] (both last read in iteration j-1).
-    {
-        const bool half_b = wave >= C::NW / 2;
-        f32x16 s[2];
-        typename T::frag pf[2][2];
-        auto mfma_phase = [&](auto par_tag, int j) __attribute__((always_inline)) {
-            constexpr int P = decltype(par_tag)::value;   // parity of j
-            if (j >= 1) pv(smem + (2 + (1 - P)) * C::TILE_BYTES, pf);
-            if (j < nt) qk(smem + P * C::TILE_BYTES, s);
-        };
-        auto iter = [&](auto par_tag, int j) __attribute__((always_inline)) {
-            constexpr int P = decltype(par_tag)::value;
-            gload_k(j + 1);
-            gload_v(j);
-            if (!half_b) mfma_phase(par_tag, j);
-            else if (j >= 1) softmax_tile(s, (j - 1) * C::BN, pf);
-            __syncthreads();
-            if (!half_b) { if (j < nt) softmax_tile(s, j * C::BN, pf); }
-            else mfma_phase(par_tag, j);
-            lds_store_k(smem + (1 - P) * C::TILE_BYTES);
-            lds_store_v(smem + (2 + P) * C::TILE_BYTES);
-            __syncthreads();
-        };
-        gload_k(0);
-        lds_store_k(smem);
-        __syncthreads();
-        for (int j = 0; j <= nt; j += 2) {
-            iter(std::integral_constant<int, 0>(), j);
-            if (j + 1 <= nt) iter(std::integral_constant<int, 1>(), j + 1);
-        }
-    }
-#else
-    // Software pipeline (T15, FA_FWD_PIPE): while the VALU runs the softmax of tile j, the matrix
-    // pipe computes S of tile j+1 (K one tile ahead of V in LDS). Plain: K[j], V[j] in buffer P.
-    f32x16 sA[2], sB[2];   // S of even / odd tiles
+    // Dense walk: K[j], V[j] in LDS buffer j & 1.
     // DMA: piece p (1 KiB = RPP rows of the tile image) is written by wave p % NW; lane l lands at
     // byte 16 l of the piece, i.e. row RPP p + l / NC, slot l % NC, which holds chunk slot ^ x(row)
     constexpr int PIECES = C::TILE_BYTES / 1024;
@@ -579,44 +451,25 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
 #endif
         }
     };
-    // stage the next K/V tiles: issue (loads) early, commit (LDS writes, or the DMA's wait) late
+    // stage the next K/V tiles: issue the DMA early, wait for it late
     auto stage_issue = [&](char *kb_wr, char *vb_wr, int jk, int jv) __attribute__((always_inline)) {
-        if constexpr (FA_FWD_DMA) {
-            dma_tile(kr, dma_k_off, k_tile_step, kb_wr, jk);
-            dma_tile(vr, dma_v_off, v_tile_step, vb_wr, jv);
-        } else {
-            gload_k(jk);
-            gload_v(jv);
-        }
+        dma_tile(kr, dma_k_off, k_tile_step, kb_wr, jk);
+        dma_tile(vr, dma_v_off, v_tile_step, vb_wr, jv);
     };
-    auto stage_commit = [&](char *kb_wr, char *vb_wr) __attribute__((always_inline)) {
-        if constexpr (FA_FWD_DMA) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            lds_store_k(kb_wr);
-            lds_store_v(vb_wr);
-        }
-    };
+    auto stage_commit = [&]() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
     auto step = [&](auto par_tag, int j) __attribute__((always_inline)) {
         constexpr int P = decltype(par_tag)::value;
-        constexpr bool PIPE = FA_FWD_PIPE;
-        f32x16 (&s)[2] = P == 0 ? sA : sB;       // this tile's scores
-        f32x16 (&sn)[2] = P == 0 ? sB : sA;      // next tile's scores
-        char *kb_rd = smem + (PIPE ? 1 - P : P) * C::TILE_BYTES;
+        char *kb_rd = smem + P * C::TILE_BYTES;
         char *vb_rd = smem + (2 + P) * C::TILE_BYTES;
-        char *kb_wr = smem + (PIPE ? P : 1 - P) * C::TILE_BYTES;
+        char *kb_wr = smem + (1 - P) * C::TILE_BYTES;
         char *vb_wr = smem + (3 - P) * C::TILE_BYTES;
-        const int kv0 = j * C::BN;
-        stage_issue(kb_wr, vb_wr, PIPE ? j + 2 : j + 1, j + 1);
-        if constexpr (!PIPE) qk(kb_rd, s);
+        stage_issue(kb_wr, vb_wr, j + 1, j + 1);
+        f32x16 s[2];
+        qk(kb_rd, s);
         typename T::frag pf[2][2];
-        if constexpr (PIPE) {
-            // split the softmax so the next tile's MFMAs overlap its exp/sum part
-            qk(kb_rd, sn);
-        }
-        softmax_tile(s, kv0, pf);
+        softmax_tile(s, j * C::BN, pf);
         pv(vb_rd, pf);
-        stage_commit(kb_wr, vb_wr);
+        stage_commit();
         __syncthreads();
     };
 
@@ -659,30 +512,23 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
             j = jn;
         }
     } else {
-        // prologue: K[0] -> kbuf0, V[0] -> vbuf0 (+ K[1] -> kbuf1 and S of tile 0 when pipelined)
+        // prologue: K[0] -> kbuf0, V[0] -> vbuf0
         stage_issue(smem, smem + 2 * C::TILE_BYTES, 0, 0);
-        stage_commit(smem, smem + 2 * C::TILE_BYTES);
-        if (FA_FWD_PIPE) {
-            gload_k(1);
-            lds_store_k(smem + C::TILE_BYTES);
-        }
+        stage_commit();
         __syncthreads();
-        if (FA_FWD_PIPE) qk(smem, sA);
         for (int j = 0; j < nt; j += 2) {
             step(std::integral_constant<int, 0>(), j);
             if (j + 1 < nt) step(std::integral_constant<int, 1>(), j + 1);
         }
     }
-#endif
 
     // ---- epilogue
-    const float l_tot = FA_FWD_MFMA_SUM ? lsum[0] : pair_sum(l_i);
+    const float l_tot = pair_sum(l_i);
     const bool empty = (l_tot == 0.f) || (l_tot != l_tot);
     float inv = empty ? 1.f : 1.f / l_tot;
     if (DROPOUT) inv *= 1.0f / (1.0f - a.p_dropout);
     if (qrow < seqlen_q) {
         uint16_t *op = (uint16_t *)a.o + (int64_t)(q_start + qrow) * a.o_row_stride + (int64_t)h * a.o_head_stride;
-#if FA_FWD_WIDE_STORE
         // 16-byte stores (T21): lanes l and l+32 hold the two 8-byte halves of each 8-column group
         // of the same row; one v_permlane32_swap per word gives lane l group g4 whole and lane
         // l+32 group g4+1 whole, so each lane writes 16 contiguous bytes instead of 2 x 8.
@@ -699,19 +545,6 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
                 const int d = 32 * dt + 8 * (g4 + hi);
                 if (d < head_dim) gstore128(op + d, u32x4{s0[0], s1[0], s0[1], s1[1]});
             }
-#else
-#pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = 32 * dt + 8 * g4 + 4 * hi;
-                if (d < head_dim) {
-                    u32x2 w = {T::pack2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv),
-                               T::pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv)};
-                    gstore64(op + d, w);
-                }
-            }
-#endif
         if (hi == 0) {
             a.softmax_lse[(int64_t)(b * a.nheads + h) * a.lse_stride + qrow] =
                 empty ? -INFINITY : (MTHR ? mc_row * LN2 : m_i * a.softmax_scale) + __logf(l_tot);

@@ -2,7 +2,6 @@
 #pragma once
 #include "fa_launch.h"
 #include "fa_fwd_kernel.h"
-#include "fa_fwd16_kernel.h"
 #include "fa_bwd_kernel.h"
 #include "fa_bwd_split_kernel.h"
 #include "fa_bwd_dq_kernel.h"
@@ -11,18 +10,38 @@
 #define FA_BWD_DQ_NW 8   // waves (32 query rows each) per dQ-pass workgroup
 #endif
 
+#include <atomic>
 #include <cstdlib>
 
 namespace fa {
+
+// Raise a kernel's dynamic-LDS limit once per (kernel, device): the attribute is per device, so
+// a process that launches on several GPUs sets it on each. `done` is the call site's own bit set
+// (one static per template instantiation); devices >= 64 are set on every launch.
+template <typename K>
+static hipError_t ensure_lds(std::atomic<uint64_t> &done, K kern, int lds) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_release);
+    return e;
+}
+#define FA_ENSURE_LDS(kern, lds)                                   \
+    do {                                                           \
+        static std::atomic<uint64_t> fa_lds_done_{0};              \
+        const hipError_t fa_e_ = ensure_lds(fa_lds_done_, kern, lds); \
+        if (fa_e_ != hipSuccess) return fa_e_;                     \
+    } while (0)
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
 static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     using C = FwdCfg<D, NW>;
     const int lds = C::lds_bytes(DROPOUT);
     auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT, NW, SPARSE>;
-    static const hipError_t attr_err =
-        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (attr_err != hipSuccess) return attr_err;
+    FA_ENSURE_LDS(kern, lds);
     dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
     hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a, bm);
     return hipGetLastError();
@@ -46,27 +65,9 @@ static int pick_fwd_waves(const FaFwdArgs &) {
     return DROPOUT && D <= 64 ? 4 : FA_FWD_NW_DEFAULT;
 }
 
-// Dense forward without dropout on 16x16x32 MFMA tiles (fa_fwd16_kernel.h), 8 waves.
-template <int D, typename T, bool CAUSAL>
-static hipError_t launch_fwd16(const FaFwdArgs &a, hipStream_t stream) {
-    using C = FwdCfg<D, 8>;
-    const int lds = C::lds_bytes(false);
-    auto kern = fa_fwd16_kernel<D, T, CAUSAL, 8>;
-    static const hipError_t attr_err =
-        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (attr_err != hipSuccess) return attr_err;
-    dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a);
-    return hipGetLastError();
-}
-
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
 static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     if (bm.mask) return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8, true>(a, bm, stream);
-    if constexpr (!DROPOUT && FA_FWD16) {
-        // one lane offset serves the K and V tile loads there, so the row strides must agree
-        if (pick_fwd_waves<D, DROPOUT>(a) == 8 && a.k_row_stride == a.v_row_stride) return launch_fwd16<D, T, CAUSAL>(a, stream);
-    }
     switch (pick_fwd_waves<D, DROPOUT>(a)) {
         case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
         case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, bm, stream);
@@ -81,18 +82,14 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
         constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
         using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL>;
         auto kern = fa_bwd_split_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
-        static const hipError_t attr_err =
-            hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
-        if (attr_err != hipSuccess) return attr_err;
+        FA_ENSURE_LDS(kern, C::LDS_BYTES);
         dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
         hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
         if constexpr (DQK) {
             constexpr int NWQ = FA_BWD_DQ_NW;
             using CQ = DqCfg<D, NWQ>;
             auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
-            static const hipError_t attr_q =
-                hipFuncSetAttribute((const void *)kq, hipFuncAttributeMaxDynamicSharedMemorySize, CQ::LDS_BYTES);
-            if (attr_q != hipSuccess) return attr_q;
+            FA_ENSURE_LDS(kq, CQ::LDS_BYTES);
             dim3 gq((a.max_seqlen_q + CQ::BM - 1) / CQ::BM, a.nheads, a.batch);
             hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a);
         }
@@ -101,18 +98,14 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
     using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value, CAUSAL>;
     constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
     auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
-    static const hipError_t attr_err =
-        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
-    if (attr_err != hipSuccess) return attr_err;
+    FA_ENSURE_LDS(kern, C::LDS_BYTES);
     dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
     hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
     if constexpr (DQK) {
         constexpr int NWQ = FA_BWD_DQ_NW;
         using CQ = DqCfg<D, NWQ>;
         auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
-        static const hipError_t attr_q =
-            hipFuncSetAttribute((const void *)kq, hipFuncAttributeMaxDynamicSharedMemorySize, CQ::LDS_BYTES);
-        if (attr_q != hipSuccess) return attr_q;
+        FA_ENSURE_LDS(kq, CQ::LDS_BYTES);
         dim3 gq((a.max_seqlen_q + CQ::BM - 1) / CQ::BM, a.nheads, a.batch);
         hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a);
     }

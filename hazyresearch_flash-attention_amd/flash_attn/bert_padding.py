@@ -27,14 +27,18 @@ def _rows(x):
             ok = False
             break
         want *= size
-    if not ok:
-        x = x.contiguous()
     row_elems = 1
     for size in inner:
         row_elems *= size
+    # rows that overlap or are broadcast (stride(0) < row, e.g. an expand along dim 0) cannot be
+    # addressed as row_stride-spaced rows: copy them out instead of clamping the stride
+    if ok and x.shape[0] > 1 and x.stride(0) < row_elems:
+        ok = False
+    if not ok:
+        x = x.contiguous()
     es = x.element_size()
     stride = x.stride(0) * es if x.shape[0] > 1 else row_elems * es
-    return x, max(stride, row_elems * es), row_elems * es
+    return x, stride, row_elems * es
 
 
 def _hip():

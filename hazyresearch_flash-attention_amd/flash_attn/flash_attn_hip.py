@@ -4,7 +4,8 @@
 (csrc/flash_attn/fmha_api.cpp:112-125, 239-241): ``[out, softmax_lse, (S_dmask)]``, and `bwd`
 the signature the reference interface calls but never bound (flash_attn/flash_attn_interface.py:31-33),
 returning ``softmax_d``. Both accept one extra keyword, ``rng_state=(seed, offset)``, so that
-the autograd layer can replay a forward's dropout mask without saving the whole RNG state.
+the autograd layer can replay a forward's dropout mask without saving the whole RNG state
+(a third element, a device word, carries the offset advance of a captured hipGraph replay).
 
 The library is loaded with ctypes (plain C ABI, include/fa_hip.h). There is no CPU fallback:
 if the shared object is missing every call raises.
@@ -29,6 +30,7 @@ FA_QUERY_BWD_ARGS_SIZE = 5
 FA_QUERY_MASK_ARGS_SIZE = 6
 FA_QUERY_PAD_WORKSPACE = 7
 FA_QUERY_ROTARY_ARGS_SIZE = 8
+FA_QUERY_BWD_WORKSPACE_NEEDED = 9
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -50,7 +52,7 @@ class FaFwdArgs(ctypes.Structure):
         ("max_seqlen_q", _i32), ("max_seqlen_k", _i32), ("lse_stride", _i32),
         ("s_rows", _i32), ("s_cols", _i32),
         ("softmax_scale", _f32), ("p_dropout", _f32),
-        ("rng_seed", _u64), ("rng_offset", _u64),
+        ("rng_seed", _u64), ("rng_offset", _u64), ("rng_offset_dev", _vp),
         ("is_causal", _i32), ("dtype", _i32),
     ]
 
@@ -73,7 +75,7 @@ class FaBwdArgs(ctypes.Structure):
         ("max_seqlen_q", _i32), ("max_seqlen_k", _i32),
         ("total_q", _i32), ("lse_stride", _i32),
         ("softmax_scale", _f32), ("p_dropout", _f32),
-        ("rng_seed", _u64), ("rng_offset", _u64),
+        ("rng_seed", _u64), ("rng_offset", _u64), ("rng_offset_dev", _vp),
         ("is_causal", _i32), ("dtype", _i32),
     ]
 
@@ -178,18 +180,87 @@ def _on_device(dev):
     return torch.cuda.device(dev)
 
 
+_rng_lock = threading.Lock()
+_graph_ctr = {}   # device index -> int64 (1,) device counter advanced by captured graphs
+
+
+def _dev_index(device):
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def _graph_counter(device):
+    """The per-device counter word that captured dropout launches advance (allocated eagerly: an
+    allocation made during capture would be re-initialised by every replay)."""
+    idx = _dev_index(device)
+    c = _graph_ctr.get(idx)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(
+                "flash_attn: dropout inside hipGraph capture needs one eager (warm-up) call of the "
+                "attention on this device before capture, as torch.cuda.graph recommends")
+        c = torch.zeros(1, dtype=torch.int64, device=torch.device("cuda", idx))
+        _graph_ctr[idx] = c
+    return c
+
+
 def reserve_rng(device, gen=None, increment=None):
     """Reserve a Philox (seed, offset) pair from the torch generator, like
-    `gen->philox_cuda_state(counter_offset)` under the generator mutex (fmha_api.cpp:228-235)."""
+    `gen->philox_cuda_state(counter_offset)` under the generator mutex (fmha_api.cpp:228-235).
+
+    Returns (seed, offset, offset_dev). offset_dev is None in eager mode. Under hipGraph capture
+    (where the reference's PhiloxCudaState reads its offset from device memory) it is a fresh
+    one-word device tensor that the captured graph sets, on every replay, from a per-device
+    counter advanced by `increment`; the kernels add it to `offset`, so each replay draws a new
+    dropout mask and the backward (which gets the same word) replays its forward's mask."""
     if increment is None:
         increment = 4
     if gen is None:
-        idx = device.index if device.index is not None else torch.cuda.current_device()
-        gen = torch.cuda.default_generators[idx]
-    seed = gen.initial_seed()
-    offset = gen.get_offset()
-    gen.set_offset(offset + increment)
-    return int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset)
+        gen = torch.cuda.default_generators[_dev_index(device)]
+    capturing = torch.cuda.is_current_stream_capturing()
+    ctr = _graph_counter(device) if capturing or _dev_index(device) not in _graph_ctr else None
+    with _rng_lock:
+        seed = gen.initial_seed()
+        offset = gen.get_offset()
+        gen.set_offset(offset + increment)
+    offset_dev = None
+    if capturing:
+        ctr.add_(increment)                       # captured: runs on every replay
+        offset_dev = torch.empty_like(ctr)        # graph-pool word owned by this call
+        offset_dev.copy_(ctr)
+    return int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset), offset_dev
+
+
+def _unpack_rng(rng_state):
+    seed, offset = rng_state[0], rng_state[1]
+    dev_word = rng_state[2] if len(rng_state) > 2 else None
+    return seed, offset, (dev_word.data_ptr() if dev_word is not None else None)
+
+
+def _rows_ok(t):
+    """True when every (row, head) slice of a (rows, H, D) tensor is its own contiguous D-run and
+    rows do not overlap: the kernels address rows through buffer descriptors sized
+    seqlen * row_stride, which a broadcast (stride 0) or overlapping row stride breaks."""
+    if t.stride(-1) != 1:
+        return False
+    n, h, d = t.shape
+    row_extent = (h - 1) * t.stride(1) + d if h > 0 else d
+    return t.stride(0) >= max(row_extent, d) and (h <= 1 or t.stride(1) >= d)
+
+
+def _rows_input(t):
+    return t if _rows_ok(t) else t.contiguous()
+
+
+_ws_needed = {}
+
+
+def _bwd_needs_workspace(head_dim, dropout, sparse):
+    key = (head_dim, bool(dropout), bool(sparse))
+    v = _ws_needed.get(key)
+    if v is None:
+        v = bool(lib().fa_query(FA_QUERY_BWD_WORKSPACE_NEEDED, head_dim, int(dropout), int(sparse)))
+        _ws_needed[key] = v
+    return v
 
 
 def _raise(rc, what):
@@ -220,6 +291,7 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
     _check(q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1, "last dimension must be contiguous")
     _check(cu_seqlens_q.is_contiguous() and cu_seqlens_k.is_contiguous(), "cu_seqlens must be contiguous")
     _check(q.dim() == 3 and k.dim() == 3 and v.dim() == 3, "q, k, v must be (total, nheads, headdim)")
+    q, k, v = _rows_input(q), _rows_input(k), _rows_input(v)
     batch = cu_seqlens_q.numel() - 1
     total_q, nheads, head_dim = q.shape
     total_k = k.shape[0]
@@ -246,9 +318,9 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
             if s is not None:
                 s.zero_()
         if p_dropout > 0.0:
-            seed, offset = rng_state if rng_state is not None else reserve_rng(dev, gen)
+            seed, offset, offset_dev = _unpack_rng(rng_state if rng_state is not None else reserve_rng(dev, gen))
         else:
-            seed, offset = 0, 0
+            seed, offset, offset_dev = 0, 0, None
         a = _args("fwd")
         a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
         a.softmax_lse = lse.data_ptr()
@@ -263,7 +335,7 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
         a.s_rows, a.s_cols = (s.shape[2], s.shape[3]) if s is not None else (0, 0)
         a.softmax_scale = float(softmax_scale)
         a.p_dropout = float(p_dropout)
-        a.rng_seed, a.rng_offset = seed, offset
+        a.rng_seed, a.rng_offset, a.rng_offset_dev = seed, offset, offset_dev
         a.is_causal = 1 if is_causal else 0
         a.dtype = dt
         if layout is None:
@@ -287,10 +359,10 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
     for t, n in ((dout, "dout"), (k, "k"), (v, "v"), (out, "out"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
         _check(t.dtype == q.dtype, f"{n} must have the dtype of q")
         _check(t.is_cuda, f"{n} must be on the GPU")
-    if dout.stride(-1) != 1:
-        dout = dout.contiguous()
-    for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
-        _check(t.stride(-1) == 1, f"{n} must have contiguous last dimension")
+    # inputs with broadcast or overlapping rows (e.g. the dout of out.sum(0)) are made contiguous
+    dout, q, k, v, out = (_rows_input(t) for t in (dout, q, k, v, out))
+    for t, n in ((dq, "dq"), (dk, "dk"), (dv, "dv")):
+        _check(_rows_ok(t), f"{n} must have contiguous last dimension and non-overlapping rows")
     _check(softmax_lse.dtype == torch.float32 and softmax_lse.is_contiguous(), "softmax_lse must be fp32 contiguous")
     batch = cu_seqlens_q.numel() - 1
     total_q, nheads, head_dim = q.shape
@@ -306,19 +378,23 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
             dk.zero_()
             dv.zero_()
         softmax_d = torch.empty((batch, nheads, lse_stride), dtype=torch.float32, device=dev)
-        dq_accum = torch.empty((total_q, nheads, head_dim), dtype=torch.float32, device=dev)
+        # the fp32 dQ workspace only exists for the atomic-dQ kernels (fa_query says which)
+        dq_accum = None
+        if _bwd_needs_workspace(head_dim, p_dropout > 0.0, layout is not None):
+            dq_accum = torch.empty((total_q, nheads, head_dim), dtype=torch.float32, device=dev)
         if p_dropout > 0.0:
             # Without rng_state, draw from the generator like the reference protocol does: the
             # caller restored the forward's RNG state (flash_attn_interface.py:60-63), so the
             # same (seed, offset) comes out again.
-            seed, offset = rng_state if rng_state is not None else reserve_rng(dev, gen)
+            seed, offset, offset_dev = _unpack_rng(rng_state if rng_state is not None else reserve_rng(dev, gen))
         else:
-            seed, offset = 0, 0
+            seed, offset, offset_dev = 0, 0, None
         a = _args("bwd")
         a.dout, a.q, a.k, a.v, a.out = dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
         a.softmax_lse = softmax_lse.data_ptr()
         a.dq, a.dk, a.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
-        a.softmax_d, a.dq_accum = softmax_d.data_ptr(), dq_accum.data_ptr()
+        a.softmax_d = softmax_d.data_ptr()
+        a.dq_accum = dq_accum.data_ptr() if dq_accum is not None else None
         a.cu_seqlens_q, a.cu_seqlens_k = cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr()
         a.do_row_stride, a.do_head_stride = dout.stride(0), dout.stride(1)
         a.q_row_stride, a.q_head_stride = q.stride(0), q.stride(1)
@@ -333,7 +409,7 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
         a.total_q, a.lse_stride = total_q, lse_stride
         a.softmax_scale = float(softmax_scale)
         a.p_dropout = float(p_dropout)
-        a.rng_seed, a.rng_offset = seed, offset
+        a.rng_seed, a.rng_offset, a.rng_offset_dev = seed, offset, offset_dev
         a.is_causal = 1 if is_causal else 0
         a.dtype = dt
         if layout is None:

@@ -28,7 +28,10 @@
  *   - Plain C types only: raw device pointers, element strides (int64), sizes. No torch types.
  *   - The caller allocates every output and workspace (the Python layer uses torch.empty).
  *   - Every call is stream-ordered and asynchronous on `stream` (a hipStream_t, NULL = default).
- *     No host synchronisation, no allocation, no exit(); safe for hipGraph capture.
+ *     No host synchronisation, no allocation, no exit(), so calls can be captured into a
+ *     hipGraph. Dropout under capture: a captured (seed, rng_offset) is a constant, so pass
+ *     rng_offset_dev pointing at a device word that the graph advances before each launch
+ *     (flash_attn_hip.py does this), or every replay draws the same mask.
  *   - Return 0 on success; non-zero = error, with a message in fa_last_error() (thread-local).
  *   - No global mutable state: concurrent calls from several host threads are safe.
  *
@@ -81,6 +84,9 @@ typedef struct FaFwdArgs {
     float p_dropout;          /* probability of DROPPING, in [0, 1) (fmha_api.cpp:99-107) */
     uint64_t rng_seed;        /* Philox key */
     uint64_t rng_offset;      /* Philox stream offset reserved from the torch generator */
+    const uint64_t *rng_offset_dev;  /* optional device word added to rng_offset when the kernel
+                                        runs (NULL = none): lets a captured hipGraph advance the
+                                        dropout stream on every replay */
     int32_t is_causal;        /* top-left aligned: col <= row (mask.h:58-72) */
     int32_t dtype;            /* FA_DTYPE_* */
 } FaFwdArgs;
@@ -99,7 +105,8 @@ typedef struct FaBwdArgs {
     void *dk;                 /* (total_k, H, D) output; may be a strided view */
     void *dv;
     float *softmax_d;         /* (B, H, lse_stride) fp32 output: rowsum(dout * out) */
-    float *dq_accum;          /* workspace: fa_query(FA_QUERY_BWD_WORKSPACE) bytes, any contents */
+    float *dq_accum;          /* workspace: fa_query(FA_QUERY_BWD_WORKSPACE) bytes, any contents;
+                                 may be NULL when fa_query(FA_QUERY_BWD_WORKSPACE_NEEDED) is 0 */
     const int32_t *cu_seqlens_q;
     const int32_t *cu_seqlens_k;
     int64_t do_row_stride, do_head_stride;
@@ -117,6 +124,7 @@ typedef struct FaBwdArgs {
     float p_dropout;
     uint64_t rng_seed;        /* must equal the forward's seed/offset to replay its dropout mask */
     uint64_t rng_offset;
+    const uint64_t *rng_offset_dev;  /* as in FaFwdArgs: must be the forward's word, unchanged since */
     int32_t is_causal;
     int32_t dtype;
 } FaBwdArgs;
@@ -194,6 +202,8 @@ enum {
     FA_QUERY_MASK_ARGS_SIZE = 6,  /* sizeof(FaBlockMask) */
     FA_QUERY_PAD_WORKSPACE = 7,   /* a = dst_rows -> bytes of fa_index_put_first_axis's workspace */
     FA_QUERY_ROTARY_ARGS_SIZE = 8,   /* sizeof(FaRotaryArgs) */
+    FA_QUERY_BWD_WORKSPACE_NEEDED = 9,   /* a = head_dim, b = (p_dropout > 0), c = block-sparse
+                                            -> 1 if fa_bwd reads dq_accum, 0 if dq is written directly */
 };
 int64_t fa_query(int what, int64_t a, int64_t b, int64_t c);
 

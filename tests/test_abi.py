@@ -62,6 +62,7 @@ def _valid_fwd_args(hip):
     ("head_dim", 60, 2), ("head_dim", 136, 2), ("batch", 0, 1), ("nheads", 0, 1), ("dtype", 7, 1),
     ("p_dropout", 1.0, 1), ("p_dropout", -0.1, 1), ("lse_stride", -1, 1), ("q", None, 1),
     ("q_row_stride", 129, 1), ("softmax_scale", float("inf"), 1),
+    ("q_row_stride", 0, 1), ("k_row_stride", 8, 1),      # broadcast / overlapping rows
 ])
 def test_fwd_argument_validation(field, value, code):
     from flash_attn import flash_attn_hip as hip
@@ -72,6 +73,58 @@ def test_fwd_argument_validation(field, value, code):
     rc = L.fa_fwd(ctypes.byref(a), None)
     assert rc == code
     assert len(L.fa_last_error()) > 0
+
+
+def _valid_bwd_args(hip):
+    a = hip.FaBwdArgs()
+    for f in ("dout", "q", "k", "v", "out", "softmax_lse", "dq", "dk", "dv", "softmax_d", "cu_seqlens_q",
+              "cu_seqlens_k"):
+        setattr(a, f, 4096)
+    for f in ("do", "q", "k", "v", "o", "dq", "dk", "dv"):
+        setattr(a, f + "_row_stride", 256)
+        setattr(a, f + "_head_stride", 128)
+    a.batch, a.nheads, a.head_dim = 1, 2, 128
+    a.max_seqlen_q = 0                      # no query rows: returns before any launch
+    a.max_seqlen_k = 16
+    a.lse_stride = 16
+    a.softmax_scale = 0.125
+    a.dtype = hip.FA_DTYPE_BF16
+    return a
+
+
+def test_bwd_workspace_query_and_validation():
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    W = hip.FA_QUERY_BWD_WORKSPACE_NEEDED
+    # D=128 dense: dq written directly (no fp32 workspace); dropout / block-sparse / D<=64: atomics
+    assert L.fa_query(W, 128, 0, 0) == 0 and L.fa_query(W, 96, 0, 0) == 0
+    assert L.fa_query(W, 128, 1, 0) == 1 and L.fa_query(W, 128, 0, 1) == 1 and L.fa_query(W, 64, 0, 0) == 1
+    assert hip._bwd_needs_workspace(128, False, False) is False
+    a = _valid_bwd_args(hip)
+    assert L.fa_bwd(ctypes.byref(a), None) == 0          # max_seqlen_q = 0: nothing to launch (no grid 0)
+    a.head_dim = 64
+    assert L.fa_bwd(ctypes.byref(a), None) == 1          # D=64 needs dq_accum
+    a.dq_accum = 4096
+    assert L.fa_bwd(ctypes.byref(a), None) == 0
+    a.do_row_stride = 0                                   # broadcast dO rows are rejected
+    assert L.fa_bwd(ctypes.byref(a), None) == 1
+    a.do_row_stride = 256
+    a.max_seqlen_k = 1 << 23                              # 2^23 rows x 256 x 2 B >= 2 GiB
+    assert L.fa_bwd(ctypes.byref(a), None) == 2
+    assert b"2 GiB" in L.fa_last_error()
+
+
+def test_rows_normalisation():
+    import torch
+    from flash_attn import flash_attn_hip as hip
+    x = torch.randn(1, 2, 64).expand(5, 2, 64)            # stride(0) == 0
+    assert not hip._rows_ok(x) and hip._rows_ok(hip._rows_input(x))
+    y = torch.randn(5, 3, 2, 64)[:, 1]                    # packed view: stride(0) = 3*2*64
+    assert hip._rows_ok(y) and hip._rows_input(y) is y
+    from flash_attn.bert_padding import _rows
+    z = torch.randn(1, 4, 8).expand(6, 4, 8)
+    zc, stride, row = _rows(z)
+    assert zc.is_contiguous() and stride == row == 4 * 8 * 4
 
 
 @pytest.mark.parametrize("rows,cols,stride,code", [

@@ -194,7 +194,7 @@ def test_dropout_mask_matches_oracle_rng(causal):
     x = make_inputs(B, S, S, H, d, torch.bfloat16, DEV, mode_q="full", mode_k="full", seed=3)
     torch.manual_seed(123)
     from flash_attn import flash_attn_hip as hip
-    seed, offset = hip.reserve_rng(torch.device(DEV))
+    seed, offset, _ = hip.reserve_rng(torch.device(DEV))
     out, lse, Sd = hip.fwd(x["q_unpad"], x["k_unpad"], x["v_unpad"], x["cu_q"], x["cu_k"], S, S, p, d ** -0.5,
                            False, causal, True, None, rng_state=(seed, offset))
     keep = torch.from_numpy(dropout_keep_mask(seed, offset, p, B, H, S, S)).to(DEV)

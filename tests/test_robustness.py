@@ -1,0 +1,118 @@
+"""GPU tests of the host-boundary edge cases: broadcast / overlapping rows, empty query sets in the
+backward, and dropout inside a captured hipGraph (the reference reserves its Philox state with the
+capture-aware philox_cuda_state, fmha_api.cpp:231-235)."""
+import pytest
+import torch
+
+from oracle.attention_ref import attention_ref, max_err_bound
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _fi():
+    from flash_attn import flash_attn_interface as fi
+    return fi
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_backward_through_broadcast_dout(d):
+    """out.sum(0) backpropagates a dout with row stride 0; dV must equal P^T dO, not zero."""
+    fi = _fi()
+    B, S, H = 2, 96, 2
+    g = torch.Generator().manual_seed(0)
+    q, k, v = [torch.randn(B * S, H, d, generator=g).bfloat16().to(DEV).requires_grad_() for _ in range(3)]
+    cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=DEV)
+    out = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
+    w = torch.randn(H, d, generator=g).bfloat16().to(DEV)
+    dq, dk, dv = torch.autograd.grad((out.sum(0) * w).sum(), (q, k, v))
+    qb, kb, vb = [t.detach().view(B, S, H, d).requires_grad_() for t in (q, k, v)]
+    ref, _ = attention_ref(qb, kb, vb)
+    pt, _ = attention_ref(qb, kb, vb, upcast=False, reorder_ops=True)
+    gout = w.expand(B, S, H, d)
+    refs = torch.autograd.grad(ref, (qb, kb, vb), gout)
+    pts = torch.autograd.grad(pt, (qb, kb, vb), gout)
+    for name, a, r, lo in zip(("dq", "dk", "dv"), (dq, dk, dv), refs, pts):
+        err = (a.view(B, S, H, d).float() - r.float()).abs().max().item()
+        assert err <= max_err_bound(lo, r), (name, err)
+    assert dv.abs().max() > 0
+
+
+def test_forward_with_expanded_kv():
+    """k/v broadcast along the token axis (stride 0): every key equal, so out == v row."""
+    fi = _fi()
+    S, H, d = 64, 2, 64
+    g = torch.Generator().manual_seed(1)
+    q = torch.randn(S, H, d, generator=g).bfloat16().to(DEV)
+    k = torch.randn(1, H, d, generator=g).bfloat16().to(DEV).expand(S, H, d)
+    v = torch.randn(1, H, d, generator=g).bfloat16().to(DEV).expand(S, H, d)
+    cu = torch.tensor([0, S], dtype=torch.int32, device=DEV)
+    out = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
+    assert torch.allclose(out.float(), v.float(), atol=1e-2)
+
+
+def test_index_first_axis_expanded_input():
+    """bert_padding gather of a row-broadcast tensor (stride(0) = 0) reads one row, not past it."""
+    from flash_attn.bert_padding import index_first_axis
+    x = torch.randn(1, 3, 16, device=DEV).bfloat16().expand(10, 3, 16)
+    idx = torch.tensor([0, 4, 9], device=DEV)
+    assert torch.equal(index_first_axis(x, idx), x[idx])
+
+
+def test_backward_with_no_query_rows():
+    """max_seqlen_q = 0: the backward is a no-op (the forward already is), no zero-size launch."""
+    fi = _fi()
+    H, d = 2, 64
+    q = torch.empty(0, H, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(5, H, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(5, H, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    cu_q = torch.tensor([0, 0], dtype=torch.int32, device=DEV)
+    cu_k = torch.tensor([0, 5], dtype=torch.int32, device=DEV)
+    out = fi.flash_attn_unpadded_func(q, k, v, cu_q, cu_k, 0, 5, 0.0)
+    assert out.shape == (0, H, d)
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), torch.empty_like(out), allow_unused=True)
+    assert dq.shape == q.shape
+
+
+def test_dropout_under_graph_capture_advances_the_stream():
+    """Two replays of a captured forward draw different dropout masks; each replay's output equals
+    an eager call at the offset the graph used (seed, offset + device word)."""
+    fi = _fi()
+    from flash_attn import flash_attn_hip as hip
+    B, S, H, d, p = 2, 128, 2, 64, 0.3
+    g = torch.Generator().manual_seed(2)
+    q, k, v = [torch.randn(B * S, H, d, generator=g).bfloat16().to(DEV) for _ in range(3)]
+    cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):   # warm-up (allocates the per-device counter word)
+            fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, p)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    state = {}
+    orig = hip.reserve_rng
+
+    def spy(*a, **kw):
+        r = orig(*a, **kw)
+        state["rng"] = r
+        return r
+
+    hip.reserve_rng = spy
+    try:
+        with torch.cuda.graph(graph):
+            out = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, p)
+    finally:
+        hip.reserve_rng = orig
+    seed, offset, word = state["rng"]
+    assert word is not None
+    outs = []
+    for _ in range(2):
+        graph.replay()
+        torch.cuda.synchronize()
+        eff = offset + int(word.item())
+        eager = hip.fwd(q, k, v, cu, cu, S, S, p, d ** -0.5, False, False, False, None, rng_state=(seed, eff))[0]
+        assert torch.equal(out, eager)
+        outs.append(out.clone())
+    assert not torch.equal(outs[0], outs[1])
