@@ -58,7 +58,9 @@ int check_common(const Args *a, const char *fn) {
         return fail(FA_ERR_INVALID_ARGUMENT, "%s: p_dropout must be in [0, 1)", fn);
     if (!std::isfinite(a->softmax_scale)) return fail(FA_ERR_INVALID_ARGUMENT, "%s: softmax_scale must be finite", fn);
     if (a->lse_stride < a->max_seqlen_q) return fail(FA_ERR_INVALID_ARGUMENT, "%s: lse_stride < max_seqlen_q", fn);
-    if (!a->q || !a->k || !a->v || !a->softmax_lse || !a->cu_seqlens_q || !a->cu_seqlens_k)
+    // empty tensors may come with NULL data: q/lse matter only with query rows, k/v only with keys too
+    const bool has_q = a->max_seqlen_q > 0, has_k = has_q && a->max_seqlen_k > 0;
+    if (!a->cu_seqlens_q || !a->cu_seqlens_k || (has_q && (!a->q || !a->softmax_lse)) || (has_k && (!a->k || !a->v)))
         return fail(FA_ERR_INVALID_ARGUMENT, "%s: NULL tensor pointer", fn);
     return FA_OK;
 }
@@ -119,7 +121,7 @@ const FaBlockMask kDense = {nullptr, 0, 0, 0};
 int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
     int rc = check_common(a, "fa_fwd");
     if (rc) return rc;
-    if (!a->o) return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: o is NULL");
+    if (!a->o && a->max_seqlen_q > 0) return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: o is NULL");
     if (!aligned16(a->q) || !aligned16(a->k) || !aligned16(a->v) || !aligned16(a->o) ||
         (a->q_row_stride | a->k_row_stride | a->v_row_stride | a->o_row_stride | a->q_head_stride |
          a->k_head_stride | a->v_head_stride | a->o_head_stride) % 8 != 0)
@@ -153,11 +155,12 @@ int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
 int bwd_impl(const FaBwdArgs *a, const FaBlockMask &bm, void *stream) {
     int rc = check_common(a, "fa_bwd");
     if (rc) return rc;
-    if (!a->dout || !a->out || !a->dq || !a->dk || !a->dv || !a->softmax_d)
+    if (a->max_seqlen_q > 0 && (!a->dout || !a->out || !a->dq || !a->softmax_d ||
+                                (a->max_seqlen_k > 0 && (!a->dk || !a->dv))))
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: NULL tensor pointer");
     // the fp32 dQ workspace is only touched when dq is not written directly
     const bool direct = fa::bwd_dq_direct(*a, bm);
-    if (!direct && !a->dq_accum)
+    if (!direct && !a->dq_accum && a->max_seqlen_q > 0)
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: dq_accum is NULL (required unless fa_query(FA_QUERY_BWD_WORKSPACE_NEEDED) is 0)");
     if (!aligned16(a->q) || !aligned16(a->k) || !aligned16(a->v) || !aligned16(a->dout) || !aligned16(a->out) ||
         !aligned16(a->dq) || !aligned16(a->dk) || !aligned16(a->dv) || (a->dq_accum && !aligned16(a->dq_accum)) ||

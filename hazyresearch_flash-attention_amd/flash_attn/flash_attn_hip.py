@@ -182,6 +182,7 @@ def _on_device(dev):
 
 _rng_lock = threading.Lock()
 _graph_ctr = {}   # device index -> int64 (1,) device counter advanced by captured graphs
+GRAPH_RNG_BASE = 1 << 33   # Philox offset of captured launches (the kernels use offset >> 2 as a 32-bit counter)
 
 
 def _dev_index(device):
@@ -218,15 +219,21 @@ def reserve_rng(device, gen=None, increment=None):
         gen = torch.cuda.default_generators[_dev_index(device)]
     capturing = torch.cuda.is_current_stream_capturing()
     ctr = _graph_counter(device) if capturing or _dev_index(device) not in _graph_ctr else None
-    with _rng_lock:
-        seed = gen.initial_seed()
-        offset = gen.get_offset()
-        gen.set_offset(offset + increment)
     offset_dev = None
     if capturing:
+        # the generator's offset cannot be read or advanced during capture: captured launches
+        # draw from their own Philox sub-stream (offset GRAPH_RNG_BASE + the device counter),
+        # disjoint from the eager offsets below 2^33
+        seed = gen.initial_seed()
+        offset = GRAPH_RNG_BASE
         ctr.add_(increment)                       # captured: runs on every replay
         offset_dev = torch.empty_like(ctr)        # graph-pool word owned by this call
         offset_dev.copy_(ctr)
+    else:
+        with _rng_lock:
+            seed = gen.initial_seed()
+            offset = gen.get_offset()
+            gen.set_offset(offset + increment)
     return int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset), offset_dev
 
 

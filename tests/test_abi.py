@@ -60,7 +60,7 @@ def _valid_fwd_args(hip):
 
 @pytest.mark.parametrize("field,value,code", [
     ("head_dim", 60, 2), ("head_dim", 136, 2), ("batch", 0, 1), ("nheads", 0, 1), ("dtype", 7, 1),
-    ("p_dropout", 1.0, 1), ("p_dropout", -0.1, 1), ("lse_stride", -1, 1), ("q", None, 1),
+    ("p_dropout", 1.0, 1), ("p_dropout", -0.1, 1), ("lse_stride", -1, 1), ("cu_seqlens_q", None, 1),
     ("q_row_stride", 129, 1), ("softmax_scale", float("inf"), 1),
     ("q_row_stride", 0, 1), ("k_row_stride", 8, 1),      # broadcast / overlapping rows
 ])
@@ -103,7 +103,10 @@ def test_bwd_workspace_query_and_validation():
     a = _valid_bwd_args(hip)
     assert L.fa_bwd(ctypes.byref(a), None) == 0          # max_seqlen_q = 0: nothing to launch (no grid 0)
     a.head_dim = 64
-    assert L.fa_bwd(ctypes.byref(a), None) == 1          # D=64 needs dq_accum
+    a.max_seqlen_q = 4
+    assert L.fa_bwd(ctypes.byref(a), None) == 1          # D=64 with query rows needs dq_accum
+    a.max_seqlen_q = 0
+    assert L.fa_bwd(ctypes.byref(a), None) == 0          # ... but not without any
     a.dq_accum = 4096
     assert L.fa_bwd(ctypes.byref(a), None) == 0
     a.do_row_stride = 0                                   # broadcast dO rows are rejected
@@ -184,6 +187,19 @@ def test_bert_padding_host_path_matches_reference_semantics():
     out, res = index_first_axis_residual(x.reshape(21, 4), idx)
     (out.sum() + 2 * res.sum()).backward()
     assert torch.equal(x.grad.reshape(21, 4)[idx], torch.full((15, 4), 3.0))
+
+
+def test_empty_tensors_may_have_null_data():
+    """torch.empty(0, ...) has a NULL data pointer: a call with no query rows (or no keys) must
+    not reject it (the reference's zero-size calls succeed)."""
+    from flash_attn import flash_attn_hip as hip
+    L = hip.lib()
+    a = _valid_fwd_args(hip)
+    a.q = a.o = a.softmax_lse = a.k = a.v = None
+    assert L.fa_fwd(ctypes.byref(a), None) == 0
+    a.max_seqlen_q = 4
+    assert L.fa_fwd(ctypes.byref(a), None) == 1     # query rows need q/o/lse
+    assert b"NULL" in L.fa_last_error()
 
 
 def test_null_args_pointer():
