@@ -19,7 +19,10 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 BUILD = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "flash_attn", "libfa_hip.so")
 
-SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_padding.hip", "fa_rotary.hip", "fa_d32.hip", "fa_d64.hip", "fa_d128.hip"]
+SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_padding.hip", "fa_rotary.hip", "fa_d32.hip", "fa_d64.hip", "fa_d128.hip",
+           "fa_fwd2.hip"]
+# per-source extra flags: the pipelined forward keeps its row sums as scalar adds
+SOURCE_FLAGS = {"fa_fwd2.hip": ["-fno-slp-vectorize"]}
 ARCH = os.environ.get("FA_OFFLOAD_ARCH", "gfx950")
 
 
@@ -56,7 +59,7 @@ def compile_one(src, force=False, extra=()):
     if not force and _newer(obj, [srcp] + _deps()):
         return obj
     lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
-    cmd = [hipcc()] + common_flags() + list(extra) + lang + ["-c", srcp, "-o", obj]
+    cmd = [hipcc()] + common_flags() + SOURCE_FLAGS.get(src, []) + list(extra) + lang + ["-c", srcp, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

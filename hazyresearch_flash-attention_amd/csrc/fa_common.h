@@ -156,6 +156,57 @@ __device__ __forceinline__ u32x4 bload128s(__amdgpu_buffer_rsrc_t r, int byte_of
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, soff, 0));
 }
 constexpr int OOB = (int)0x80000000;  // any offset past num_records reads as zero
+
+// ---- LDS-DMA issued as inline asm (buffer_load_dwordx4 ... lds). Through the builtin, hipcc
+// orders every later ds_read_b64_tr_b16 behind an s_waitcnt vmcnt(0) for the in-flight DMA, so a
+// tile prefetched at the top of a step is waited for at that step's first V^T read; issued here the
+// DMA is invisible to the compiler's counters and the caller waits itself (vmcnt + barrier).
+#ifndef FA_DMA_ASM
+#define FA_DMA_ASM 1
+#endif
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+// wave-uniform buffer descriptor words (base, stride 0, num_records, raw-buffer flags) in SGPRs
+__device__ __forceinline__ i32x4 make_srd(const void *base, int num_bytes) {
+    const uint64_t p = (uint64_t)base;
+    i32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+    r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));
+    r[2] = __builtin_amdgcn_readfirstlane(num_bytes);
+    r[3] = 0x00020000;
+    return r;
+}
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p;
+}
+// s_waitcnt vmcnt(0) that the compiler's counters see (it then knows its own loads are done too)
+__device__ __forceinline__ void vmcnt0() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+    asm volatile("" ::: "memory");
+}
+// s_waitcnt vmcnt(N): all but the N youngest vector-memory operations done (N compile-time)
+template <int N>
+__device__ __forceinline__ void vmcnt_n() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+    asm volatile("" ::: "memory");
+}
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>());
+        static_for<B + 1, E>(f);
+    }
+}
+// one 1-KiB piece: lane l's 16 bytes from srd[voff + soff] land at LDS byte lds + 16 l
+__device__ __forceinline__ void dma16(i32x4 srd, int voff, int soff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(srd), "s"(soff), "s"(__builtin_amdgcn_readfirstlane(lds))
+                 : "memory");
+}
 __device__ __forceinline__ float bload32f(__amdgpu_buffer_rsrc_t r, int byte_off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }

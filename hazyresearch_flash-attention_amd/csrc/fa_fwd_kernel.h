@@ -439,24 +439,38 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
         dma_k_off[i] = ok ? (r * (int)a.k_row_stride + c * 8) * 2 : OOB;
         dma_v_off[i] = ok ? (r * (int)a.v_row_stride + c * 8) * 2 : OOB;
     }
-    auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, const int (&off)[PPW], int step_bytes, char *buf, int j)
-        __attribute__((always_inline)) {
+#if FA_DMA_ASM
+    const i32x4 ksrd = make_srd(kbase, n_end * (int)a.k_row_stride * 2);
+    const i32x4 vsrd = make_srd(vbase, n_end * (int)a.v_row_stride * 2);
+#endif
+    auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, const i32x4 &srd, const int (&off)[PPW], int step_bytes, char *buf,
+                        int j) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < PPW; ++i) {
             const int p = wave + NW * i;
 #if defined(__HIP_DEVICE_COMPILE__)   // (the host pass would drop the kernel's launch stub over it)
-            if (PIECES % NW == 0 || p < PIECES)
+            if (PIECES % NW == 0 || p < PIECES) {
+#if FA_DMA_ASM
+                dma16(srd, off[i], j * step_bytes, lds_addr(buf + 1024 * p));
+#else
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(buf + 1024 * p), 16,
                                                          off[i], j * step_bytes, 0, 0);
+#endif
+            }
 #endif
         }
     };
     // stage the next K/V tiles: issue the DMA early, wait for it late
     auto stage_issue = [&](char *kb_wr, char *vb_wr, int jk, int jv) __attribute__((always_inline)) {
-        dma_tile(kr, dma_k_off, k_tile_step, kb_wr, jk);
-        dma_tile(vr, dma_v_off, v_tile_step, vb_wr, jv);
+#if FA_DMA_ASM
+        dma_tile(kr, ksrd, dma_k_off, k_tile_step, kb_wr, jk);
+        dma_tile(vr, vsrd, dma_v_off, v_tile_step, vb_wr, jv);
+#else
+        dma_tile(kr, i32x4{}, dma_k_off, k_tile_step, kb_wr, jk);
+        dma_tile(vr, i32x4{}, dma_v_off, v_tile_step, vb_wr, jv);
+#endif
     };
-    auto stage_commit = [&]() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+    auto stage_commit = [&]() __attribute__((always_inline)) { vmcnt0(); };
     auto step = [&](auto par_tag, int j) __attribute__((always_inline)) {
         constexpr int P = decltype(par_tag)::value;
         char *kb_rd = smem + P * C::TILE_BYTES;

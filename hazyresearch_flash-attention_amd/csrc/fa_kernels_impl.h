@@ -10,31 +10,10 @@
 #define FA_BWD_DQ_NW 8   // waves (32 query rows each) per dQ-pass workgroup
 #endif
 
-#include <atomic>
 #include <cstdlib>
 
 namespace fa {
 
-// Raise a kernel's dynamic-LDS limit once per (kernel, device): the attribute is per device, so
-// a process that launches on several GPUs sets it on each. `done` is the call site's own bit set
-// (one static per template instantiation); devices >= 64 are set on every launch.
-template <typename K>
-static hipError_t ensure_lds(std::atomic<uint64_t> &done, K kern, int lds) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    const uint64_t bit = dev < 64 ? 1ull << dev : 0;
-    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
-    e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_release);
-    return e;
-}
-#define FA_ENSURE_LDS(kern, lds)                                   \
-    do {                                                           \
-        static std::atomic<uint64_t> fa_lds_done_{0};              \
-        const hipError_t fa_e_ = ensure_lds(fa_lds_done_, kern, lds); \
-        if (fa_e_ != hipSuccess) return fa_e_;                     \
-    } while (0)
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
 static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
@@ -65,9 +44,27 @@ static int pick_fwd_waves(const FaFwdArgs &) {
     return DROPOUT && D <= 64 ? 4 : FA_FWD_NW_DEFAULT;
 }
 
+#ifndef FA_FWD2_TILES
+#define FA_FWD2_TILES 0x2   // head-dim tiles on the pipelined dense kernel: bit 0 = 32, 1 = 64, 2 = 128
+#endif
+// Dense forward without dropout: fa_fwd2_kernel (two 32-row blocks per wave, max-free softmax).
+// FA_FWD2=0|1 in the environment overrides the per-tile default for A/B runs.
+template <int D>
+static bool use_fwd2() {
+    static const int forced = [] {
+        const char *e = getenv("FA_FWD2");
+        return e ? atoi(e) : -1;
+    }();
+    if (forced >= 0) return forced != 0;
+    return (FA_FWD2_TILES >> (D == 32 ? 0 : D == 64 ? 1 : 2)) & 1;
+}
+
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
 static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     if (bm.mask) return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8, true>(a, bm, stream);
+    if constexpr (!DROPOUT) {
+        if (use_fwd2<D>()) return launch_fwd2<D>(a, stream);   // fa_fwd2.hip
+    }
     switch (pick_fwd_waves<D, DROPOUT>(a)) {
         case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
         case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, bm, stream);

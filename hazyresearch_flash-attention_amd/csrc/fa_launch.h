@@ -1,12 +1,15 @@
 // fa_launch.h — host launchers for the gfx950 kernels (one translation unit per head-dim tile).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include "../../include/fa_hip.h"
 
 namespace fa {
 // D is the padded head-dim tile (32, 64 or 128); the kernels zero-fill head_dim < D.
 // bm.mask == nullptr: dense; otherwise the block-sparse kernels (fa_fwd_block / fa_bwd_block).
 template <int D> hipError_t launch_fwd(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
+template <int D> hipError_t launch_fwd2(const FaFwdArgs &a, hipStream_t stream);   // dense, no dropout
 template <int D> hipError_t launch_bwd(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
 hipError_t launch_probs(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
 hipError_t launch_gather_rows(const void *src, int64_t src_rows, int64_t src_stride, const int64_t *idx, int64_t n,
@@ -35,4 +38,25 @@ inline bool bwd_dq_direct(const FaBwdArgs &a, const FaBlockMask &bm) {
     return bwd_dqk_tile(tile) && a.p_dropout == 0.f && bm.mask == nullptr && a.max_seqlen_k > 0;
 }
 hipError_t launch_bwd_post(const FaBwdArgs &a, hipStream_t stream);
+
+// Raise a kernel's dynamic-LDS limit once per (kernel, device): the attribute is per device, so
+// a process that launches on several GPUs sets it on each. `done` is the call site's own bit set
+// (one static per template instantiation); devices >= 64 are set on every launch.
+template <typename K>
+static hipError_t ensure_lds(std::atomic<uint64_t> &done, K kern, int lds) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_release);
+    return e;
+}
+#define FA_ENSURE_LDS(kern, lds)                                   \
+    do {                                                           \
+        static std::atomic<uint64_t> fa_lds_done_{0};              \
+        const hipError_t fa_e_ = ensure_lds(fa_lds_done_, kern, lds); \
+        if (fa_e_ != hipSuccess) return fa_e_;                     \
+    } while (0)
 }  // namespace fa

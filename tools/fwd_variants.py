@@ -21,13 +21,17 @@ sys.path.insert(0, PKG)
 BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
-    "base": {},
-    "noxcd": {"FA_BWD_XCD": 0},
+    "base": {"FA_FWD2_TILES": 0},
+    "f2": {},
 }
+# more variants from the environment: FA_VARIANTS='{"name": {"MACRO": value, "-flag": 1}}'
+VARIANTS.update(json.loads(os.environ.get("FA_VARIANTS", "{}")))
 
 CONFIGS = [
     # name, B, H, Sq, Sk, D, causal, dtype
     ("ns_B8_H12_S2048_D64", 8, 12, 2048, 2048, 64, False, "bf16"),
+    ("xs_B16_H12_S2048_D64", 16, 12, 2048, 2048, 64, False, "bf16"),   # 1536 workgroups: whole rounds
+    ("xs_B4_H12_S2048_D64", 4, 12, 2048, 2048, 64, False, "bf16"),     # 384 workgroups
     ("c4_B16_H12_S4096_D128_causal", 16, 12, 4096, 4096, 128, True, "bf16"),
     ("c5_B4_H16_1024x4096_D64", 4, 16, 1024, 4096, 64, False, "bf16"),
     ("bs_localglobal_B8_H12_S2048_D64", 8, 12, 2048, 2048, 64, False, "bf16"),   # fa_fwd_block
@@ -42,15 +46,19 @@ def build(names):
     fb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(fb)
     fb.build(verbose=False)
-    shared = [os.path.join(BUILD, s + ".o") for s in fb.SOURCES if not s.startswith("fa_d")]
+    VAR_TUS = ("fa_d32.hip", "fa_d64.hip", "fa_d128.hip", "fa_fwd2.hip")
+    shared = [os.path.join(BUILD, s + ".o") for s in fb.SOURCES if s not in VAR_TUS]
 
     def one(name):
         defs = VARIANTS[name]
-        extra = [k if k.startswith("-") else f"-D{k}={v}" for k, v in defs.items()]
+        extra = []
+        for k, v in defs.items():
+            extra += k.split() if k.startswith("-") else [f"-D{k}={v}"]
         objs = []
-        for tu in ("fa_d32.hip", "fa_d64.hip", "fa_d128.hip"):
+        for tu in VAR_TUS:
             obj = os.path.join(BUILD, f"var_{name}_{tu}.o")
-            cmd = [fb.hipcc()] + fb.common_flags() + extra + ["-x", "hip", "-c", os.path.join(fb.CSRC, tu), "-o", obj]
+            cmd = ([fb.hipcc()] + fb.common_flags() + fb.SOURCE_FLAGS.get(tu, []) + extra +
+                   ["-x", "hip", "-c", os.path.join(fb.CSRC, tu), "-o", obj])
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode:
                 raise RuntimeError(r.stderr)
@@ -79,7 +87,10 @@ def run(names, rounds, iters):
         L.fa_fwd_block.restype = ctypes.c_int
         libs[n] = L
     results = {}
+    only_cfg = os.environ.get("FA_CONFIGS", "")
     for (cname, B, H, Sq, Sk, D, causal, dt, *pdrop) in CONFIGS:
+        if only_cfg and not any(cname.startswith(c) for c in only_cfg.split(",")):
+            continue
         p = pdrop[0] if pdrop else 0.0
         dtype = torch.bfloat16 if dt == "bf16" else torch.float16
         g = torch.Generator().manual_seed(0)
