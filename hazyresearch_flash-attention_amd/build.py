@@ -19,10 +19,8 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 BUILD = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "flash_attn", "libfa_hip.so")
 
-SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_padding.hip", "fa_rotary.hip", "fa_d32.hip", "fa_d64.hip", "fa_d128.hip",
-           "fa_fwd2.hip"]
-# per-source extra flags: the pipelined forward keeps its row sums as scalar adds
-SOURCE_FLAGS = {"fa_fwd2.hip": ["-fno-slp-vectorize"]}
+SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_padding.hip", "fa_rotary.hip", "fa_d32.hip", "fa_d64.hip", "fa_d128.hip"]
+SOURCE_FLAGS = {}   # per-source extra compiler flags
 ARCH = os.environ.get("FA_OFFLOAD_ARCH", "gfx950")
 
 

@@ -44,27 +44,9 @@ static int pick_fwd_waves(const FaFwdArgs &) {
     return DROPOUT && D <= 64 ? 4 : FA_FWD_NW_DEFAULT;
 }
 
-#ifndef FA_FWD2_TILES
-#define FA_FWD2_TILES 0x2   // head-dim tiles on the pipelined dense kernel: bit 0 = 32, 1 = 64, 2 = 128
-#endif
-// Dense forward without dropout: fa_fwd2_kernel (two 32-row blocks per wave, max-free softmax).
-// FA_FWD2=0|1 in the environment overrides the per-tile default for A/B runs.
-template <int D>
-static bool use_fwd2() {
-    static const int forced = [] {
-        const char *e = getenv("FA_FWD2");
-        return e ? atoi(e) : -1;
-    }();
-    if (forced >= 0) return forced != 0;
-    return (FA_FWD2_TILES >> (D == 32 ? 0 : D == 64 ? 1 : 2)) & 1;
-}
-
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
 static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     if (bm.mask) return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8, true>(a, bm, stream);
-    if constexpr (!DROPOUT) {
-        if (use_fwd2<D>()) return launch_fwd2<D>(a, stream);   // fa_fwd2.hip
-    }
     switch (pick_fwd_waves<D, DROPOUT>(a)) {
         case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
         case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, bm, stream);

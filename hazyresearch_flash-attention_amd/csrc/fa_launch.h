@@ -9,7 +9,6 @@ namespace fa {
 // D is the padded head-dim tile (32, 64 or 128); the kernels zero-fill head_dim < D.
 // bm.mask == nullptr: dense; otherwise the block-sparse kernels (fa_fwd_block / fa_bwd_block).
 template <int D> hipError_t launch_fwd(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
-template <int D> hipError_t launch_fwd2(const FaFwdArgs &a, hipStream_t stream);   // dense, no dropout
 template <int D> hipError_t launch_bwd(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
 hipError_t launch_probs(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream);
 hipError_t launch_gather_rows(const void *src, int64_t src_rows, int64_t src_stride, const int64_t *idx, int64_t n,

@@ -21,8 +21,7 @@ sys.path.insert(0, PKG)
 BUILD = os.path.join(PKG, "build")
 
 VARIANTS = {
-    "base": {"FA_FWD2_TILES": 0},
-    "f2": {},
+    "base": {},
 }
 # more variants from the environment: FA_VARIANTS='{"name": {"MACRO": value, "-flag": 1}}'
 VARIANTS.update(json.loads(os.environ.get("FA_VARIANTS", "{}")))
@@ -46,7 +45,7 @@ def build(names):
     fb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(fb)
     fb.build(verbose=False)
-    VAR_TUS = ("fa_d32.hip", "fa_d64.hip", "fa_d128.hip", "fa_fwd2.hip")
+    VAR_TUS = ("fa_d32.hip", "fa_d64.hip", "fa_d128.hip")
     shared = [os.path.join(BUILD, s + ".o") for s in fb.SOURCES if s not in VAR_TUS]
 
     def one(name):
