@@ -131,6 +131,15 @@ int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: row strides must be >= head_dim (no overlapping/broadcast rows)");
     if (a->s_dmask && (a->s_rows < a->max_seqlen_q || a->s_cols < a->max_seqlen_k))
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: s_dmask extents smaller than max_seqlen");
+    if (a->rot_cos || a->rot_sin) {
+        if (!a->rot_cos || !a->rot_sin || !aligned16(a->rot_cos) || !aligned16(a->rot_sin) || a->rot_stride % 8 != 0 ||
+            a->rot_stride < a->head_dim)
+            return fail(FA_ERR_INVALID_ARGUMENT,
+                        "fa_fwd: rotary tables must both be set, 16-byte aligned, rot_stride >= head_dim and a multiple of 8");
+        if (a->s_dmask) return fail(FA_ERR_UNSUPPORTED, "fa_fwd: fused rotary cannot return the attention probabilities");
+        if ((int64_t)a->max_seqlen_q * a->rot_stride * 2 >= ((int64_t)1 << 31))
+            return fail(FA_ERR_UNSUPPORTED, "fa_fwd: rotary tables span more than 2 GiB");
+    }
     // the forward addresses each sequence through 32-bit buffer offsets
     const int64_t lim = (int64_t)1 << 31;
     if ((int64_t)a->max_seqlen_q * a->q_row_stride * 2 >= lim || (int64_t)a->max_seqlen_k * a->k_row_stride * 2 >= lim ||

@@ -225,6 +225,37 @@ __device__ __forceinline__ float pair_sum(float x) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Rotary embedding of 8 consecutive features (4 interleaved pairs) of one row, rounded like torch's
+// eager evaluation of flash_attn/rotary.py:31-41 (every product and the sum rounded to T):
+//   forward  y0 = rnd(rnd(x0 c0) + rnd(-x1 s0)),  y1 = rnd(rnd(x1 c1) + rnd(x0 s1))
+//   inverse  y0 = rnd(rnd(x0 c0) + rnd(x1 s1)),   y1 = rnd(rnd(x1 c1) + rnd(-(x0 s0)))   (autograd)
+// Shared by fa_rotary (separate pass) and the Q load of fa_fwd_kernel so both give the same bits.
+// ---------------------------------------------------------------------------------------
+template <typename T, bool INVERSE>
+__device__ __forceinline__ u32x4 rotary8(u32x4 xv, u32x4 cv, u32x4 sv) {
+    // no contraction: a fused multiply-add would round once less than torch's mul, mul, add
+#pragma clang fp contract(off)
+    u32x4 out;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const float x0 = T::to_float((uint16_t)(xv[w] & 0xFFFF)), x1 = T::to_float((uint16_t)(xv[w] >> 16));
+        const float c0 = T::to_float((uint16_t)(cv[w] & 0xFFFF)), c1 = T::to_float((uint16_t)(cv[w] >> 16));
+        const float s0 = T::to_float((uint16_t)(sv[w] & 0xFFFF)), s1 = T::to_float((uint16_t)(sv[w] >> 16));
+        auto rnd = [](float v) { return T::to_float(T::from_float(v)); };
+        float y0, y1;
+        if (!INVERSE) {
+            y0 = rnd(x0 * c0) + rnd(-x1 * s0);
+            y1 = rnd(x1 * c1) + rnd(x0 * s1);
+        } else {
+            y0 = rnd(x0 * c0) + rnd(x1 * s1);
+            y1 = rnd(x1 * c1) + rnd(-(x0 * s0));
+        }
+        out[w] = T::pack2(y0, y1);
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------------------------------
 // Dropout RNG: Philox-4x32 with 7 rounds (6 keyed rounds + final), the generator of the
 // reference (csrc/flash_attn/src/philox.cuh:30-59, 121-136), used as a pure counter-based
 // function of (seed, offset, bh, row, col) so forward and backward agree under any tiling:

@@ -24,9 +24,6 @@ namespace fa {
 
 template <typename T, bool INVERSE>
 __global__ __launch_bounds__(256) void rotary_kernel(const FaRotaryArgs a) {
-    // No contraction: once hipcc shrinks the fp16 chain to half arithmetic it would otherwise fuse
-    // a product into the sum (one rounding fewer than torch's eager mul, mul, add).
-#pragma clang fp contract(off)
     const int chunks = a.head_dim / 8;
     const int64_t rows = (int64_t)a.batch * a.seqlen * a.nslot * a.nheads;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -50,27 +47,7 @@ __global__ __launch_bounds__(256) void rotary_kernel(const FaRotaryArgs a) {
     }
     const u32x4 cv = *reinterpret_cast<const u32x4 *>((const uint16_t *)a.cos + s * a.table_stride + 8 * c);
     const u32x4 sv = *reinterpret_cast<const u32x4 *>((const uint16_t *)a.sin + s * a.table_stride + 8 * c);
-    u32x4 out;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        // one 32-bit word = one pair (x0, x1) with its cos/sin (equal within the pair for the
-        // reference tables, but read per element as the tables are given)
-        const float x0 = T::to_float((uint16_t)(xv[w] & 0xFFFF)), x1 = T::to_float((uint16_t)(xv[w] >> 16));
-        const float c0 = T::to_float((uint16_t)(cv[w] & 0xFFFF)), c1 = T::to_float((uint16_t)(cv[w] >> 16));
-        const float s0 = T::to_float((uint16_t)(sv[w] & 0xFFFF)), s1 = T::to_float((uint16_t)(sv[w] >> 16));
-        float y0, y1;
-        auto rnd = [](float v) { return T::to_float(T::from_float(v)); };
-        if (!INVERSE) {
-            y0 = rnd(x0 * c0) + rnd(-x1 * s0);
-            y1 = rnd(x1 * c1) + rnd(x0 * s1);
-        } else {
-            // autograd of y = x*cos + rotate_half(x)*sin: grad of x*cos is g*cos; grad through
-            // rotate_half(x)*sin is rotate_half^T(g*sin): (g1*s1, -g0*s0)
-            y0 = rnd(x0 * c0) + rnd(x1 * s1);
-            y1 = rnd(x1 * c1) + rnd(-(x0 * s0));
-        }
-        out[w] = T::pack2(y0, y1);
-    }
+    const u32x4 out = rotary8<T, INVERSE>(xv, cv, sv);
     *reinterpret_cast<u32x4 *>(yp) = out;
 }
 

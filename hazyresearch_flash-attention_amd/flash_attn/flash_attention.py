@@ -53,6 +53,54 @@ class FlashAttention(nn.Module):
         return out.reshape(batch, seqlen, nheads, -1), None
 
 
+class FlashAttnRotaryQKVFunc(torch.autograd.Function):
+    """Attention over a padded, contiguous qkv (B, S, 3, H, D) with rotary embeddings fused into
+    the forward (README.md:56 "Fuse rotary embedding"; rotation = rotary.py:31-41):
+    * forward: k is rotated by one fa_rotary pass into a (B, S, H, D) buffer (the backward needs it
+      anyway); q is rotated by fa_fwd at its one-time fragment load, never written to HBM. The
+      operands are bit-identical to rotating q and k first (same rounding, fa_common.h rotary8).
+    * backward: q is rotated once more (fa_rotary), the attention backward runs on (q_rot, k_rot,
+      v), and dq, dk are rotated back in place (the autograd transpose, fa_rotary inverse)."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, dropout_p, softmax_scale, causal):
+        from flash_attn import flash_attn_hip as hip
+        from flash_attn.flash_attn_interface import _reserve
+        B, S, _, H, D = qkv.shape
+        assert qkv.is_contiguous()
+        cos, sin = cos[:S].contiguous(), sin[:S].contiguous()
+        st = (S * 3 * H * D, 3 * H * D, 0, D)
+        k_rot = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
+        hip.rotary(qkv[:, :, 1], k_rot, cos, sin, (B, S, 1, H, D), st, (S * H * D, H * D, 0, D), 1, False)
+        if softmax_scale is None:
+            softmax_scale = D ** (-0.5)
+        rng_state = _reserve(dropout_p, qkv.device)
+        flat = qkv.view(B * S, 3, H, D)
+        cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=qkv.device)
+        out, lse = hip.fwd(flat[:, 0], k_rot.view(B * S, H, D), flat[:, 2], cu, cu, S, S, dropout_p, softmax_scale,
+                           False, causal, False, None, rng_state=rng_state, rotary=(cos, sin))
+        ctx.save_for_backward(qkv, k_rot, out, lse, cos, sin, cu)
+        ctx.rng_state, ctx.dropout_p, ctx.softmax_scale, ctx.causal = rng_state, dropout_p, softmax_scale, causal
+        return out.view(B, S, H, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        from flash_attn import flash_attn_hip as hip
+        qkv, k_rot, out, lse, cos, sin, cu = ctx.saved_tensors
+        B, S, _, H, D = qkv.shape
+        st = (S * 3 * H * D, 3 * H * D, 0, D)
+        q_rot = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
+        hip.rotary(qkv[:, :, 0], q_rot, cos, sin, (B, S, 1, H, D), st, (S * H * D, H * D, 0, D), 1, False)
+        dqkv = torch.empty_like(qkv)
+        d = dqkv.view(B * S, 3, H, D)
+        hip.bwd(dout.reshape(B * S, H, D), q_rot.view(B * S, H, D), k_rot.view(B * S, H, D),
+                qkv.view(B * S, 3, H, D)[:, 2], out, lse, d[:, 0], d[:, 1], d[:, 2], cu, cu, S, S, ctx.dropout_p,
+                ctx.softmax_scale, False, ctx.causal, None, rng_state=ctx.rng_state)
+        st3 = (S * 3 * H * D, 3 * H * D, H * D, D)
+        hip.rotary(dqkv, dqkv, cos, sin, (B, S, 3, H, D), st3, st3, 2, True)   # dq, dk back; dv as is
+        return dqkv, None, None, None, None, None
+
+
 class FlashMHA(nn.Module):
     """Multi-head attention block: Wqkv -> optional rotary -> FlashAttention -> out_proj."""
 
@@ -81,6 +129,14 @@ class FlashMHA(nn.Module):
         """x: (batch, seqlen, embed_dim); key_padding_mask: (batch, seqlen) bool."""
         qkv = self.Wqkv(x)
         b, s = qkv.shape[0], qkv.shape[1]
+        if (self.use_rotary_emb and qkv.is_cuda and qkv.is_contiguous() and key_padding_mask is None
+                and qkv.dtype in (torch.float16, torch.bfloat16)):
+            # fused rotary: q rotated inside the attention kernel, k by one half-size pass
+            cos, sin = self.rotary_emb.cos_sin_tables(s, qkv.device, qkv.dtype)
+            dropout_p = self.inner_attn.dropout_p if self.inner_attn.training else 0.0
+            context = FlashAttnRotaryQKVFunc.apply(qkv.view(b, s, 3, self.num_heads, self.head_dim), cos, sin,
+                                                   dropout_p, self.inner_attn.softmax_scale, self.causal)
+            return self.out_proj(context.reshape(b, s, -1)), None
         if self.use_rotary_emb and qkv.is_cuda and qkv.is_contiguous():
             # q and k rotated in place in the packed projection (fa_rotary): no unbind/stack copies
             cos, sin = self.rotary_emb.cos_sin_tables(s, qkv.device, qkv.dtype)

@@ -54,6 +54,7 @@ class FaFwdArgs(ctypes.Structure):
         ("softmax_scale", _f32), ("p_dropout", _f32),
         ("rng_seed", _u64), ("rng_offset", _u64), ("rng_offset_dev", _vp),
         ("is_causal", _i32), ("dtype", _i32),
+        ("rot_cos", _vp), ("rot_sin", _vp), ("rot_stride", _i64),
     ]
 
 
@@ -287,9 +288,11 @@ def _mask_struct(layout, dev):
 
 
 def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropout, softmax_scale,
-        zero_tensors, is_causal, return_softmax, gen, rng_state=None, layout=None):
+        zero_tensors, is_causal, return_softmax, gen, rng_state=None, layout=None, rotary=None):
     """Forward pass; same arguments and result as the reference's `flash_attn_cuda.fwd`.
-    `layout` (optional, 0/1 (seqlen/16, seqlen/256) on the device) selects the block-sparse kernel."""
+    `layout` (optional, 0/1 (seqlen/16, seqlen/256) on the device) selects the block-sparse kernel.
+    `rotary` (optional (cos, sin) tables, (>= max_seqlen_q, >= D) in q's dtype) rotates q inside
+    the kernel at its load (fused rotary, rotary.py:31-41); k must come rotated already."""
     dt = _dtype_code(q.dtype)
     _check(k.dtype == q.dtype and v.dtype == q.dtype, "q, k, v must have the same dtype")
     _check(cu_seqlens_q.dtype == torch.int32 and cu_seqlens_k.dtype == torch.int32, "cu_seqlens must be int32")
@@ -345,6 +348,16 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
         a.rng_seed, a.rng_offset, a.rng_offset_dev = seed, offset, offset_dev
         a.is_causal = 1 if is_causal else 0
         a.dtype = dt
+        a.rot_cos = a.rot_sin = None
+        a.rot_stride = 0
+        if rotary is not None:
+            cos, sin = rotary
+            _check(cos.dtype == q.dtype and sin.dtype == q.dtype and cos.is_cuda and sin.is_cuda,
+                   "rotary tables must be on the GPU in q's dtype")
+            _check(cos.dim() == 2 and cos.stride(-1) == 1 and cos.stride() == sin.stride() and cos.shape == sin.shape
+                   and cos.shape[0] >= max_seqlen_q and cos.shape[1] >= head_dim,
+                   "rotary tables must be (>= max_seqlen_q, >= head_dim) with one row stride")
+            a.rot_cos, a.rot_sin, a.rot_stride = cos.data_ptr(), sin.data_ptr(), cos.stride(0)
         if layout is None:
             rc = lib().fa_fwd(ctypes.byref(a), _stream_ptr(dev))
         else:

@@ -89,6 +89,14 @@ typedef struct FaFwdArgs {
                                         dropout stream on every replay */
     int32_t is_causal;        /* top-left aligned: col <= row (mask.h:58-72) */
     int32_t dtype;            /* FA_DTYPE_* */
+    /* Optional rotary embedding fused into the Q load (flash_attn/rotary.py:31-41, README.md:56
+     * "Fuse rotary embedding"): when rot_cos != NULL, row r of each query sequence is rotated
+     * with table row r before QK^T, rounded exactly as fa_rotary's separate pass (so the result
+     * equals fa_rotary followed by fa_fwd bit for bit). k must already be rotated. Tables are
+     * (>= max_seqlen_q, rot_stride) in q's dtype, rot_stride >= head_dim. NULL = off. */
+    const void *rot_cos;
+    const void *rot_sin;
+    int64_t rot_stride;
 } FaFwdArgs;
 
 /* Backward arguments. Mirrors the bwd call made by flash_attn_interface.py:31-33:

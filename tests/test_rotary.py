@@ -1,9 +1,11 @@
 """GPU parity of the HIP rotary embedding (csrc/fa_rotary.hip) with the
-reference's torch expression (flash_attn/rotary.py:22-41, 86-135): bit-exact forward and
+oracle's restatement of the reference rotary (oracle/rotary_ref.py of flash_attn/rotary.py:22-41, 86-135): bit-exact forward and
 backward (same rounding sequence), 1-D and 2-D tables, both sequence layouts, and the in-place
 packed-qkv form used by FlashMHA."""
 import pytest
 import torch
+
+from oracle.rotary_ref import apply_rotary_ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -27,8 +29,8 @@ def test_rotary_1d_bitexact(D, seq_dimension, dtype):
     emb = rot.RotaryEmbedding(D).to(DEV)
     qh, kh = emb(q, k, seq_dimension=seq_dimension)
     cos, sin = emb.cos_sin_tables(S, DEV, dtype)
-    qt = rot._apply_rotary_torch(q, cos, sin, seq_dimension)
-    kt = rot._apply_rotary_torch(k, cos, sin, seq_dimension)
+    qt = apply_rotary_ref(q, cos, sin, seq_dimension)
+    kt = apply_rotary_ref(k, cos, sin, seq_dimension)
     assert torch.equal(qh, qt) and torch.equal(kh, kt)
     go = torch.randn(qh.shape, generator=g).to(dtype).to(DEV)
     (gq_h,) = torch.autograd.grad(qh, (q,), go)
@@ -55,10 +57,10 @@ def test_rotary_2d_bitexact(seq_dimension, dtype):
     c1, s1 = emb.rotary_emb1d.cos_sin_tables(side, DEV, dtype)
     q0, q1 = qq.chunk(2, dim=-1)
     k0, k1 = kk.chunk(2, dim=-1)
-    qt = torch.cat([flat(rot._apply_rotary_torch(grid(q0), c1, s1, -2)),
-                    flat(rot._apply_rotary_torch(grid(q1), c1, s1, -3))], dim=-1)
-    kt = torch.cat([flat(rot._apply_rotary_torch(grid(k0), c1, s1, -2)),
-                    flat(rot._apply_rotary_torch(grid(k1), c1, s1, -3))], dim=-1)
+    qt = torch.cat([flat(apply_rotary_ref(grid(q0), c1, s1, -2)),
+                    flat(apply_rotary_ref(grid(q1), c1, s1, -3))], dim=-1)
+    kt = torch.cat([flat(apply_rotary_ref(grid(k0), c1, s1, -2)),
+                    flat(apply_rotary_ref(grid(k1), c1, s1, -3))], dim=-1)
     if seq_dimension == -3:
         qt, kt = qt.transpose(1, 2), kt.transpose(1, 2)
     assert torch.equal(qh, qt) and torch.equal(kh, kt)
@@ -79,7 +81,7 @@ def test_rotary_qkv_inplace(kind, dtype):
     out = rot.apply_rotary_emb_qkv_(base, cos, sin, H, D).reshape(B, S, 3, H, D)
     ref_in = (w * 1.0).reshape(B, S, 3, H, D)
     q, k, v = ref_in.unbind(dim=2)
-    ref = torch.stack([rot._apply_rotary_torch(q, cos, sin, -3), rot._apply_rotary_torch(k, cos, sin, -3), v], dim=2)
+    ref = torch.stack([apply_rotary_ref(q, cos, sin, -3), apply_rotary_ref(k, cos, sin, -3), v], dim=2)
     assert torch.equal(out, ref)
     go = torch.randn(out.shape, generator=g).to(dtype).to(DEV)
     assert torch.equal(torch.autograd.grad(out, (w,), go)[0], torch.autograd.grad(ref, (w,), go)[0])
