@@ -245,7 +245,19 @@ def main():
         rbytes = 2 * 2 * 8 * 2048 * 12 * 64 * 2
         extra["rotary_qkv_inplace_B8_S2048_H12_D64_bf16"] = {
             "ms": round(ms_r, 4), "GBps": round(rbytes / ms_r / 1e6, 1), "frac_hbm": round(rbytes / ms_r / 1e6 / PEAK_HBM_GBS, 4)}
-        del qkv_r
+        # rotary fused into the attention forward (FlashMHA's path: q rotated at the kernel's Q load,
+        # k by a half-size pass) against the separate q+k pass followed by the plain forward
+        from flash_attn.flash_attention import FlashAttnRotaryQKVFunc
+        from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func
+        qkv5 = qkv_r.view(8, 2048, 3, 12, 64)
+        cu_r = torch.arange(0, 9 * 2048, 2048, dtype=torch.int32, device=dev)
+        ms_sep, _ = time_events(lambda: flash_attn_unpadded_qkvpacked_func(
+            apply_rotary_emb_qkv_(qkv_r, rc, rs, 12, 64).view(8 * 2048, 3, 12, 64), cu_r, 2048, 0.0), 20, 20)
+        ms_fus, _ = time_events(lambda: FlashAttnRotaryQKVFunc.apply(qkv5, rc, rs, 0.0, None, False), 20, 20)
+        extra["rotary_attention_fwd_B8_S2048_H12_D64_bf16"] = {
+            "separate_pass_ms": round(ms_sep, 4), "fused_q_ms": round(ms_fus, 4),
+            "speedup": round(ms_sep / ms_fus, 3)}
+        del qkv_r, qkv5
         # C3 forward + backward (the fwd+bwd headline of the reference README charts)
         q3, k3, v3, _, c3q, c3k = make_inputs(8, 12, 2048, 2048, 64, torch.bfloat16, dev)
         q3.requires_grad_(); k3.requires_grad_(); v3.requires_grad_()

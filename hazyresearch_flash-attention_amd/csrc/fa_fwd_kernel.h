@@ -30,9 +30,6 @@
 
 namespace fa {
 
-#ifndef FA_FWD_ROTK
-#define FA_FWD_ROTK 0   // 1: A/B variant that also rotates k in the kernel (fa_fwd expects rotated k)
-#endif
 // Register budget of the block-sparse kernels without dropout (waves per SIMD).
 #ifndef FA_FWD_SPARSE_WPE
 #define FA_FWD_SPARSE_WPE 4
@@ -305,22 +302,14 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
             }
 
     // S^T = K Q^T for one 64-key tile: two 32x32 sub-tiles, lane = query row, registers = keys
-    auto qk = [&](const char *kb, f32x16 (&s)[2], int kv0) __attribute__((always_inline)) {
+    auto qk = [&](const char *kb, f32x16 (&s)[2]) __attribute__((always_inline)) {
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) s[st][r] = 0.f;
 #pragma unroll
             for (int ks = 0; ks < D / 16; ++ks) {
-                u32x4 kw = lds_read128(kb, k_rd[st][ks]);
-#if FA_FWD_ROTK   // A/B variant only: k rotated at every fragment read instead of by a pre-pass
-                if (rot) {
-                    const int key = kv0 + 32 * st + l32, c = 2 * ks + hi;
-                    const int to = key < seqlen_k && c * 8 < head_dim ? (key * (int)a.rot_stride + c * 8) * 2 : OOB;
-                    kw = rotary8<T, false>(kw, bload128(rcos, to), bload128(rsin, to));
-                }
-#endif
-                s[st] = T::mfma32(as_frag<T>(kw), qf[ks], s[st]);
+                s[st] = T::mfma32(as_frag<T>(lds_read128(kb, k_rd[st][ks])), qf[ks], s[st]);
             }
         }
     };
@@ -499,7 +488,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
         char *vb_wr = smem + (3 - P) * C::TILE_BYTES;
         stage_issue(kb_wr, vb_wr, j + 1, j + 1);
         f32x16 s[2];
-        qk(kb_rd, s, j * C::BN);
+        qk(kb_rd, s);
         typename T::frag pf[2][2];
         softmax_tile(s, j * C::BN, pf);
         pv(vb_rd, pf);
@@ -521,7 +510,7 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
             const bool lane_live = (lane_cols >> (j >> 2)) & 1;
             if (__builtin_amdgcn_ballot_w64(lane_live)) {
                 f32x16 s[2];
-                qk(kb_rd, s, j * C::BN);
+                qk(kb_rd, s);
                 typename T::frag pf[2][2];
                 softmax_tile(s, j * C::BN, pf);
                 pv(vb_rd, pf);

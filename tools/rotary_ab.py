@@ -2,9 +2,11 @@
 
   separate  : fa_rotary rotates q and k of the packed qkv in place, then fa_fwd
   fused_q   : fa_rotary rotates k only (half the bytes), fa_fwd rotates q at its fragment load
-  fused_qk  : no pass; fa_fwd (variant library built with FA_FWD_ROTK=1) also rotates every K
-              fragment it reads from LDS (python tools/fwd_variants.py build --only rotk with
-              FA_VARIANTS='{"rotk": {"FA_FWD_ROTK": 1}}')
+  fused_qk  : no pass; fa_fwd also rotates every K fragment it reads from LDS. That variant
+              (FA_FWD_ROTK in fa_fwd_kernel.h) lost 3x and was removed; it lives in the commit
+              "Rotary fused into the forward's Q load". Build var_rotk.so from that commit with
+              FA_VARIANTS='{"rotk": {"FA_FWD_ROTK": 1}}' tools/fwd_variants.py build --only rotk
+              to re-run the leg; without the library it is skipped.
 
     python tools/rotary_ab.py [--B 8 --S 2048 --H 12 --D 64]     (GPU; prints one JSON line)
 """
