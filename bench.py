@@ -288,6 +288,27 @@ def main():
         del q4, k4, v4, gout4
 
     if not args.no_extra and rank == 0:
+        # the reference benchmark script's own configuration (benchmarks/benchmark_flash_attention.py:39-70):
+        # B=64 H=16 S=1024 D=64 fp16, dropout 0.1, random right padding (lengths 1004..1023), unpadded
+        # qkv, non-causal; forward and forward+backward of flash_attn_unpadded_qkvpacked_func
+        from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func as _qkvf
+        gb = torch.Generator(device="cpu").manual_seed(0)
+        lens = torch.randint(1024 - 20, 1024, (64,), generator=gb)
+        cu_b = torch.zeros(65, dtype=torch.int32)
+        cu_b[1:] = torch.cumsum(lens, 0)
+        cu_b = cu_b.to(dev)
+        nnz = int(lens.sum())
+        qkv_b = torch.randn(nnz, 3, 16, 64, generator=gb).half().to(dev).requires_grad_()
+        go_b = torch.randn(nnz, 16, 64, generator=gb).half().to(dev)
+        ms_bf, _ = time_events(lambda: _qkvf(qkv_b, cu_b, 1024, 0.1), 10, 20)
+        ms_bfb, _ = time_events(lambda: torch.autograd.grad(_qkvf(qkv_b, cu_b, 1024, 0.1), (qkv_b,), go_b), 5, 10)
+        fl_b = float((4.0 * 16 * 64 * lens.double() ** 2).sum())
+        extra["ref_benchmark_B64_H16_S1024_D64_fp16_p0.1_padded"] = {
+            "fwd_ms": round(ms_bf, 4), "fwd_TFLOPS": round(fl_b / ms_bf / 1e9, 2),
+            "fwd_bwd_ms": round(ms_bfb, 4), "fwd_bwd_TFLOPS": round(3.5 * fl_b / ms_bfb / 1e9, 2)}
+        del qkv_b, go_b
+
+    if not args.no_extra and rank == 0:
         # the reference's published metric (README.md:69-81): fwd+bwd speedup over PyTorch standard
         # attention at B=8 H=12 D=64 fp16, S=2048, no mask / no dropout (tools/speedup_vs_pytorch.py
         # sweeps S and the mask/dropout cases into profiles/)
