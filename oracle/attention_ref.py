@@ -102,6 +102,13 @@ def max_err_bound(out_pt, out_ref, floor=0.0):
     return max(2 * (out_pt.float() - out_ref.float()).abs().max().item(), floor)
 
 
+def ulp_floor(ref, dtype=torch.bfloat16):
+    """One unit of the output dtype's last place at the reference's magnitude: the floor of the
+    2x rule where the low-precision baseline happens to be exact (1-key rows, tiny sequences)."""
+    eps = torch.finfo(dtype).eps
+    return float(ref.float().abs().max().item()) * eps
+
+
 def attention_blocksparse_ref(qkv, blockmask, attn_mask=None, dropout_p=0.0, dropout_mask=None, causal=False,
                               upcast=True, reorder_ops=False):
     """qkv (B, S, 3, H, D); blockmask (S/16 rounded up, S/256 rounded up) 0/1, entry [r][c] lets

@@ -15,7 +15,7 @@ import pytest
 import torch
 
 from fa_testutil import convert_s_dmask, make_inputs
-from oracle.attention_ref import attention_ref, get_dropout_fraction, max_err_bound, pad
+from oracle.attention_ref import attention_ref, get_dropout_fraction, max_err_bound, pad, ulp_floor
 from oracle.philox import dropout_keep_mask
 
 pytestmark = pytest.mark.gpu
@@ -160,9 +160,12 @@ def test_flash_attn_reference_grid(layout, seqlen, d, dropout_p, causal, dtype):
 @pytest.mark.parametrize("dropout_p", [0.0, 0.17])
 def test_flash_attn_race_condition(seqlen, d, dropout_p, causal, dtype):
     """Determinism (tests/test_flash_attn.py:610-671): 10 reruns with the same seed give bit-identical
-    outputs, probabilities and (here enabled) gradients. dQ is summed with fp32 atomics, so it is
-    compared with a tolerance of 1 ulp-scale instead of bitwise."""
+    outputs, probabilities and (here enabled) gradients. dQ is bitwise too where the query-major dQ
+    pass writes it (D=128, no dropout); the atomic-dQ kernels sum it with fp32 atomics in a varying
+    order, so there it may differ by one unit in the last place of the output dtype."""
     fi = _fa()
+    from flash_attn import flash_attn_hip as hip
+    atomic_dq = hip._bwd_needs_workspace(d, dropout_p > 0, False)
     x = make_inputs(8, seqlen, seqlen, 4, d, dtype, DEV, seed=0)
     q_u = x["q_unpad"].detach().requires_grad_()
     k_u = x["k_unpad"].detach().requires_grad_()
@@ -183,7 +186,13 @@ def test_flash_attn_race_condition(seqlen, d, dropout_p, causal, dtype):
         assert torch.equal(S, ref[1])
         assert torch.equal(dk, ref[3])
         assert torch.equal(dv, ref[4])
-        assert torch.allclose(dq.float(), ref[2].float(), rtol=1e-2, atol=1e-3)
+        if atomic_dq:
+            # fp32 atomics: the summation order of dQ varies, so the bf16/fp16 output may round to
+            # the neighbouring value: at most one unit in the last place of the output dtype
+            eps = torch.finfo(dtype).eps
+            torch.testing.assert_close(dq.float(), ref[2].float(), rtol=eps, atol=eps * 1e-3)
+        else:
+            assert torch.equal(dq, ref[2])   # query-major dQ pass writes dq directly: bitwise
 
 
 @pytest.mark.parametrize("causal", [False, True])
@@ -249,7 +258,7 @@ def test_empty_and_ragged_sequences():
         ref, _ = attention_ref(q[qs][None], k[ks][None], v[ks][None])
         pt, _ = attention_ref(q[qs][None], k[ks][None], v[ks][None], upcast=False, reorder_ops=True)
         err = (out[qs].float() - ref[0].float()).abs().max().item()
-        assert err <= max_err_bound(pt, ref, floor=1e-2), (b, err)
+        assert err <= max_err_bound(pt, ref, floor=ulp_floor(ref)), (b, err)
 
 
 @pytest.mark.parametrize("causal", [False, True])
@@ -286,7 +295,9 @@ def test_empty_and_ragged_sequences_backward(d, causal):
         pts = torch.autograd.grad(pt, (qb, kb, vb), gout[qs][None])
         for name, a, r, lo in zip(("dq", "dk", "dv"), (dq[qs], dk[ks], dv[ks]), refs, pts):
             err = (a.float() - r[0].float()).abs().max().item()
-            assert err <= max_err_bound(lo, r, floor=1e-2), (b, name, err)
+            # a 1-key row has dq = 0 exactly in fp32, while the kernel's dP - delta cancels to
+            # fp32 rounding residue (~1e-6): the floor is one output ulp, at least 1e-5
+            assert err <= max_err_bound(lo, r, floor=max(ulp_floor(r), 1e-5)), (b, name, err)
 
 
 def test_invalid_arguments_raise():

@@ -36,6 +36,7 @@ CONFIGS = [
     ("bs_localglobal_B8_H12_S2048_D64", 8, 12, 2048, 2048, 64, False, "bf16"),   # fa_fwd_block
     ("c2_B8_H12_S512_D64_fp16", 8, 12, 512, 512, 64, False, "fp16"),
     ("c3_B8_H12_S2048_D64_causal_p0.1", 8, 12, 2048, 2048, 64, True, "bf16", 0.1),
+    ("c3nd_B8_H12_S2048_D64_causal", 8, 12, 2048, 2048, 64, True, "bf16", 0.0),
 ]
 
 
@@ -180,7 +181,10 @@ def run_bwd(names, rounds, iters):
         L.fa_bwd.restype = ctypes.c_int
         libs[n] = L
     results = {}
+    only_cfg = os.environ.get("FA_CONFIGS", "")
     for (cname, B, H, S, D, causal, p) in BWD_CONFIGS:
+        if only_cfg and not any(cname.startswith(c) for c in only_cfg.split(",")):
+            continue
         g = torch.Generator().manual_seed(0)
         q, k, v, do = (torch.randn(B * S, H, D, generator=g).bfloat16().cuda() for _ in range(4))
         cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device="cuda")
