@@ -269,15 +269,30 @@ __device__ __forceinline__ u32x4 rotary8(u32x4 xv, u32x4 cv, u32x4 sv) {
 // One Philox call serves the 8 rows {16s+4h+0..3, 16s+8+4h+0..3} of one column: exactly the
 // registers 8s..8s+7 of a 32x32 accumulator whose lane is the column (the backward's layout).
 // ---------------------------------------------------------------------------------------
+#ifndef FA_PHILOX_XOR3
+#define FA_PHILOX_XOR3 1   // 1: each round's two 3-input XORs as one v_bitop3_b32 (gfx950)
+#endif
+// a ^ b ^ k with k wave-uniform (a Philox key word): one v_bitop3_b32 (truth table 0x96 = XOR3)
+// instead of two v_xor_b32; hipcc does not form it from the C expression.
+__device__ __forceinline__ uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) {
+#if FA_PHILOX_XOR3 && defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(__builtin_amdgcn_readfirstlane(k)));
+    return r;
+#else
+    return a ^ b ^ k;
+#endif
+}
+
 __device__ __forceinline__ u32x4 philox7(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                         uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
         uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n0 = xor3_key((uint32_t)(p1 >> 32), c1, k0);
         uint32_t n1 = (uint32_t)p1;
-        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n2 = xor3_key((uint32_t)(p0 >> 32), c3, k1);
         uint32_t n3 = (uint32_t)p0;
         c0 = n0; c1 = n1; c2 = n2; c3 = n3;
         k0 += 0x9E3779B9u;
