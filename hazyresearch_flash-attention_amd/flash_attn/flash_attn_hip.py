@@ -14,6 +14,7 @@ import contextlib
 import ctypes
 import math
 import os
+import struct
 import threading
 
 import torch
@@ -158,8 +159,50 @@ def _round16(x):
     return (x + 15) // 16 * 16
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream_ptr(device):
+    if _raw_stream is not None:
+        return _raw_stream(device.index if device.index is not None else torch.cuda.current_device())
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def _packer(cls):
+    """A struct.Struct whose layout equals the ctypes mirror `cls` (explicit padding), so a call
+    fills the whole argument block with one pack_into instead of one ctypes setattr per field."""
+    codes = {_vp: "Q", _i64: "q", _i32: "i", _u64: "Q", _f32: "f"}
+    fmt, off = "<", 0
+    for name, typ in cls._fields_:
+        o = getattr(cls, name).offset
+        if o > off:
+            fmt += f"{o - off}x"
+        fmt += codes[typ]
+        off = o + ctypes.sizeof(typ)
+    if ctypes.sizeof(cls) > off:
+        fmt += f"{ctypes.sizeof(cls) - off}x"
+    st = struct.Struct(fmt)
+    assert st.size == ctypes.sizeof(cls)
+    return st
+
+
+_fwd_packer = None
+
+
+def _fwd_call():
+    """(packer, per-thread argument buffer, its address, raw fa_fwd taking the address)."""
+    global _fwd_packer
+    c = getattr(_tls, "fwd_raw", None)
+    if c is None:
+        if _fwd_packer is None:
+            _fwd_packer = _packer(FaFwdArgs)
+        buf = ctypes.create_string_buffer(_fwd_packer.size)
+        fn = lib()["fa_fwd"]            # a second prototype of the same symbol, taking the address
+        fn.argtypes = [_vp, _vp]
+        fn.restype = ctypes.c_int
+        c = (_fwd_packer, buf, ctypes.addressof(buf), fn)
+        _tls.fwd_raw = c
+    return c
 
 
 _tls = threading.local()
@@ -293,21 +336,32 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
     `layout` (optional, 0/1 (seqlen/16, seqlen/256) on the device) selects the block-sparse kernel.
     `rotary` (optional (cos, sin) tables, (>= max_seqlen_q, >= D) in q's dtype) rotates q inside
     the kernel at its load (fused rotary, rotary.py:31-41); k must come rotated already."""
-    dt = _dtype_code(q.dtype)
-    _check(k.dtype == q.dtype and v.dtype == q.dtype, "q, k, v must have the same dtype")
+    qdt = q.dtype
+    dt = _dtype_code(qdt)
+    _check(k.dtype == qdt and v.dtype == qdt, "q, k, v must have the same dtype")
     _check(cu_seqlens_q.dtype == torch.int32 and cu_seqlens_k.dtype == torch.int32, "cu_seqlens must be int32")
     _check(q.is_cuda and k.is_cuda and v.is_cuda and cu_seqlens_q.is_cuda and cu_seqlens_k.is_cuda,
            "all tensors must be on the GPU")
-    _check(q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1, "last dimension must be contiguous")
-    _check(cu_seqlens_q.is_contiguous() and cu_seqlens_k.is_contiguous(), "cu_seqlens must be contiguous")
     _check(q.dim() == 3 and k.dim() == 3 and v.dim() == 3, "q, k, v must be (total, nheads, headdim)")
-    q, k, v = _rows_input(q), _rows_input(k), _rows_input(v)
+    qs, ks, vs = q.stride(), k.stride(), v.stride()
+    _check(qs[2] == 1 and ks[2] == 1 and vs[2] == 1, "last dimension must be contiguous")
+    _check(cu_seqlens_q.is_contiguous() and cu_seqlens_k.is_contiguous(), "cu_seqlens must be contiguous")
+    if not _rows_ok(q):
+        q = q.contiguous()
+        qs = q.stride()
+    if not _rows_ok(k):
+        k = k.contiguous()
+        ks = k.stride()
+    if not _rows_ok(v):
+        v = v.contiguous()
+        vs = v.stride()
     batch = cu_seqlens_q.numel() - 1
     total_q, nheads, head_dim = q.shape
-    total_k = k.shape[0]
+    kshape = k.shape
+    total_k = kshape[0]
     _check(batch > 0, "batch_size must be positive")
     _check(head_dim % 8 == 0 and head_dim <= 128, "head_size must be a multiple of 8 and <= 128")
-    _check(tuple(k.shape) == (total_k, nheads, head_dim) and tuple(v.shape) == (total_k, nheads, head_dim),
+    _check(tuple(kshape) == (total_k, nheads, head_dim) and tuple(v.shape) == (total_k, nheads, head_dim),
            "k, v must have shape (total_k, nheads, headdim)")
     _check(cu_seqlens_k.numel() == batch + 1, "cu_seqlens_k must have shape (batch_size + 1)")
     _check(0.0 <= p_dropout < 1.0, "dropout_p must be in [0, 1)")
@@ -316,12 +370,12 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
     dev = q.device
 
     with _on_device(dev):
-        o = torch.empty((total_q, nheads, head_dim), dtype=q.dtype, device=dev)
+        o = torch.empty((total_q, nheads, head_dim), dtype=qdt, device=dev)
         lse_stride = max(_round16(max_seqlen_q), 16)
         lse = torch.empty((batch, nheads, lse_stride), dtype=torch.float32, device=dev)
         s = None
         if return_softmax:
-            s = torch.empty((batch, nheads, lse_stride, max(_round16(max_seqlen_k), 16)), dtype=q.dtype, device=dev)
+            s = torch.empty((batch, nheads, lse_stride, max(_round16(max_seqlen_k), 16)), dtype=qdt, device=dev)
         if zero_tensors:
             o.zero_()
             lse.fill_(-math.inf)
@@ -331,36 +385,31 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
             seed, offset, offset_dev = _unpack_rng(rng_state if rng_state is not None else reserve_rng(dev, gen))
         else:
             seed, offset, offset_dev = 0, 0, None
-        a = _args("fwd")
-        a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
-        a.softmax_lse = lse.data_ptr()
-        a.s_dmask = s.data_ptr() if s is not None else None
-        a.cu_seqlens_q, a.cu_seqlens_k = cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr()
-        a.q_row_stride, a.q_head_stride = q.stride(0), q.stride(1)
-        a.k_row_stride, a.k_head_stride = k.stride(0), k.stride(1)
-        a.v_row_stride, a.v_head_stride = v.stride(0), v.stride(1)
-        a.o_row_stride, a.o_head_stride = o.stride(0), o.stride(1)
-        a.batch, a.nheads, a.head_dim = batch, nheads, head_dim
-        a.max_seqlen_q, a.max_seqlen_k, a.lse_stride = max_seqlen_q, max_seqlen_k, lse_stride
-        a.s_rows, a.s_cols = (s.shape[2], s.shape[3]) if s is not None else (0, 0)
-        a.softmax_scale = float(softmax_scale)
-        a.p_dropout = float(p_dropout)
-        a.rng_seed, a.rng_offset, a.rng_offset_dev = seed, offset, offset_dev
-        a.is_causal = 1 if is_causal else 0
-        a.dtype = dt
-        a.rot_cos = a.rot_sin = None
-        a.rot_stride = 0
+        rot_cos = rot_sin = 0
+        rot_stride = 0
         if rotary is not None:
             cos, sin = rotary
-            _check(cos.dtype == q.dtype and sin.dtype == q.dtype and cos.is_cuda and sin.is_cuda,
+            _check(cos.dtype == qdt and sin.dtype == qdt and cos.is_cuda and sin.is_cuda,
                    "rotary tables must be on the GPU in q's dtype")
             _check(cos.dim() == 2 and cos.stride(-1) == 1 and cos.stride() == sin.stride() and cos.shape == sin.shape
                    and cos.shape[0] >= max_seqlen_q and cos.shape[1] >= head_dim,
                    "rotary tables must be (>= max_seqlen_q, >= head_dim) with one row stride")
-            a.rot_cos, a.rot_sin, a.rot_stride = cos.data_ptr(), sin.data_ptr(), cos.stride(0)
+            rot_cos, rot_sin, rot_stride = cos.data_ptr(), sin.data_ptr(), cos.stride(0)
+        # FaFwdArgs field order (include/fa_hip.h), packed in one call
+        packer, buf, addr, raw_fwd = _fwd_call()
+        nh_d = nheads * head_dim
+        packer.pack_into(
+            buf, 0, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
+            s.data_ptr() if s is not None else 0, cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr(),
+            qs[0], qs[1], ks[0], ks[1], vs[0], vs[1], nh_d, head_dim,
+            batch, nheads, head_dim, max_seqlen_q, max_seqlen_k, lse_stride,
+            s.shape[2] if s is not None else 0, s.shape[3] if s is not None else 0,
+            float(softmax_scale), float(p_dropout), seed, offset, offset_dev or 0,
+            1 if is_causal else 0, dt, rot_cos, rot_sin, rot_stride)
         if layout is None:
-            rc = lib().fa_fwd(ctypes.byref(a), _stream_ptr(dev))
+            rc = raw_fwd(addr, _stream_ptr(dev))
         else:
+            a = FaFwdArgs.from_buffer_copy(buf)
             m, _keep = _mask_struct(layout, dev)
             rc = lib().fa_fwd_block(ctypes.byref(a), ctypes.byref(m), _stream_ptr(dev))
         if rc != 0:

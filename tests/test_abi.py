@@ -189,6 +189,32 @@ def test_bert_padding_host_path_matches_reference_semantics():
     assert torch.equal(x.grad.reshape(21, 4)[idx], torch.full((15, 4), 3.0))
 
 
+def test_fwd_packer_matches_ctypes_layout():
+    """The one-call struct.pack_into image of FaFwdArgs (flash_attn_hip._fwd_call) is byte-identical
+    to the ctypes mirror filled field by field (whose size fa_query checks against the C header)."""
+    import random
+    from flash_attn import flash_attn_hip as hip
+    packer = hip._packer(hip.FaFwdArgs)
+    rnd = random.Random(1)
+    a = hip.FaFwdArgs()
+    vals = []
+    for name, typ in hip.FaFwdArgs._fields_:
+        if typ is ctypes.c_float:
+            v = rnd.random()
+            v = ctypes.c_float(v).value
+        elif typ is ctypes.c_int32:
+            v = rnd.randint(-2 ** 31, 2 ** 31 - 1)
+        elif typ is ctypes.c_int64:
+            v = rnd.randint(-2 ** 63, 2 ** 63 - 1)
+        else:
+            v = rnd.randint(0, 2 ** 64 - 1)
+        setattr(a, name, v)
+        vals.append(v)
+    buf = ctypes.create_string_buffer(packer.size)
+    packer.pack_into(buf, 0, *vals)
+    assert bytes(buf) == bytes(a)
+
+
 def test_empty_tensors_may_have_null_data():
     """torch.empty(0, ...) has a NULL data pointer: a call with no query rows (or no keys) must
     not reject it (the reference's zero-size calls succeed)."""
