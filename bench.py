@@ -29,6 +29,9 @@ import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 flop/clk x 2.4 GHz, dense (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+# what a bare v_mfma_f32_32x32x16_bf16 stream sustains on random operands on this chip
+# (tools/micro/mfma_rate.hip, profiles/r02_mfma_ceiling.txt): the clock drops under random-data load
+MFMA_CEILING_RANDOM_TFLOPS = 1845.0
 CLOCK_WARMUP_S = 0.25   # untimed, time-based warm-up before every timed region
 
 
@@ -180,6 +183,8 @@ def main():
     achieved = flops / (avg_ms * 1e-3) / 1e12
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": read_traffic(),
+                "measured_mfma_ceiling": MFMA_CEILING_RANDOM_TFLOPS,
+                "frac_of_measured_ceiling": round(achieved / MFMA_CEILING_RANDOM_TFLOPS, 4),
                 "kernel": "fa_fwd_kernel<64,bf16,noncausal,nodropout>", "avg_kernel_ms": round(avg_ms, 4),
                 "flops_per_launch": flops, "algorithmic_bytes_per_launch": fwd_bytes(B, H, S, S, D)}
 
