@@ -167,6 +167,7 @@ BWD_CONFIGS = [
     ("bwd_ns_B8_H12_S2048_D32", 8, 12, 2048, 32, False, 0.0),
     ("bwd_ns_B8_H12_S2048_D128", 8, 12, 2048, 128, False, 0.0),
     ("bwd_c_B8_H12_S2048_D128_causal", 8, 12, 2048, 128, True, 0.0),
+    ("bwd_c4_B16_H12_S4096_D128_causal", 16, 12, 4096, 128, True, 0.0),
 ]
 
 
