@@ -40,9 +40,6 @@ namespace fa {
 #ifndef FA_BWD_FULLTILE
 #define FA_BWD_FULLTILE 1       // 1: unguarded dQ atomics on full query tiles
 #endif
-#ifndef FA_BWD_ATOMIC_LATE
-#define FA_BWD_ATOMIC_LATE 1    // 1: dQ atomics issued after the prefetched query tile's LDS write
-#endif
 #ifndef FA_BWD_DQ_PREFETCH
 #define FA_BWD_DQ_PREFETCH 1    // 1: dQ MFMA operands read one key step ahead
 #endif
@@ -506,11 +503,10 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                         }
                     }
                     const int d = dbase + (lane & 15);
-#if FA_BWD_ATOMIC_LATE
                     // the prefetched query tile goes to LDS first: its vmcnt wait then covers only
-                    // loads, and these atomics have a whole tile of compute before the next wait
+                    // loads (vmcnt retires in issue order), and these atomics have a whole tile of
+                    // compute before the next wait
                     if (t0 == 0 && itn < nqt) lds_store_qtile(1 - BUF);
-#endif
                     if (FA_BWD_FULLTILE && q0 + C::BQ <= seqlen_q && head_dim == D) {
                         // full tile (wave-uniform test): the four atomics without per-lane guards
                         float *base = dqa + (int64_t)(q0 + 16 * qh + 4 * g4) * dqa_row + d;
@@ -526,12 +522,8 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                 }
             }
         }
-#if FA_BWD_ATOMIC_LATE
         // waves without a dQ tile (or kernels without dQ) store the prefetched tile here
         if (itn < nqt && (!DQ || wave >= 2 * (D / 16))) lds_store_qtile(1 - BUF);
-#else
-        if (itn < nqt) lds_store_qtile(1 - BUF);
-#endif
         __syncthreads();
     };
     if constexpr (SPARSE) {

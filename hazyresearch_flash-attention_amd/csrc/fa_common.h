@@ -161,9 +161,6 @@ constexpr int OOB = (int)0x80000000;  // any offset past num_records reads as ze
 // orders every later ds_read_b64_tr_b16 behind an s_waitcnt vmcnt(0) for the in-flight DMA, so a
 // tile prefetched at the top of a step is waited for at that step's first V^T read; issued here the
 // DMA is invisible to the compiler's counters and the caller waits itself (vmcnt + barrier).
-#ifndef FA_DMA_ASM
-#define FA_DMA_ASM 1
-#endif
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 // wave-uniform buffer descriptor words (base, stride 0, num_records, raw-buffer flags) in SGPRs
 __device__ __forceinline__ i32x4 make_srd(const void *base, int num_bytes) {
@@ -200,12 +197,14 @@ __device__ __forceinline__ void static_for(F &&f) {
 }
 // one 1-KiB piece: lane l's 16 bytes from srd[voff + soff] land at LDS byte lds + 16 l
 __device__ __forceinline__ void dma16(i32x4 srd, int voff, int soff, uint32_t lds) {
+#if defined(__HIP_DEVICE_COMPILE__)   // (the host pass never runs it)
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
                  "buffer_load_dwordx4 %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(voff), "s"(srd), "s"(soff), "s"(__builtin_amdgcn_readfirstlane(lds))
                  : "memory");
+#endif
 }
 __device__ __forceinline__ float bload32f(__amdgpu_buffer_rsrc_t r, int byte_off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
@@ -269,13 +268,10 @@ __device__ __forceinline__ u32x4 rotary8(u32x4 xv, u32x4 cv, u32x4 sv) {
 // One Philox call serves the 8 rows {16s+4h+0..3, 16s+8+4h+0..3} of one column: exactly the
 // registers 8s..8s+7 of a 32x32 accumulator whose lane is the column (the backward's layout).
 // ---------------------------------------------------------------------------------------
-#ifndef FA_PHILOX_XOR3
-#define FA_PHILOX_XOR3 1   // 1: each round's two 3-input XORs as one v_bitop3_b32 (gfx950)
-#endif
 // a ^ b ^ k with k wave-uniform (a Philox key word): one v_bitop3_b32 (truth table 0x96 = XOR3)
 // instead of two v_xor_b32; hipcc does not form it from the C expression.
 __device__ __forceinline__ uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) {
-#if FA_PHILOX_XOR3 && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     uint32_t r;
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(__builtin_amdgcn_readfirstlane(k)));
     return r;

@@ -448,36 +448,22 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
         dma_k_off[i] = ok ? (r * (int)a.k_row_stride + c * 8) * 2 : OOB;
         dma_v_off[i] = ok ? (r * (int)a.v_row_stride + c * 8) * 2 : OOB;
     }
-#if FA_DMA_ASM
+    // LDS-DMA through inline asm (fa_common.h dma16): through the builtin, hipcc put an
+    // s_waitcnt vmcnt(0) for the in-flight DMA in front of the first ds_read_b64_tr_b16 of every tile
     const i32x4 ksrd = make_srd(kbase, n_end * (int)a.k_row_stride * 2);
     const i32x4 vsrd = make_srd(vbase, n_end * (int)a.v_row_stride * 2);
-#endif
-    auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, const i32x4 &srd, const int (&off)[PPW], int step_bytes, char *buf,
-                        int j) __attribute__((always_inline)) {
+    auto dma_tile = [&](const i32x4 &srd, const int (&off)[PPW], int step_bytes, char *buf, int j)
+        __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < PPW; ++i) {
             const int p = wave + NW * i;
-#if defined(__HIP_DEVICE_COMPILE__)   // (the host pass would drop the kernel's launch stub over it)
-            if (PIECES % NW == 0 || p < PIECES) {
-#if FA_DMA_ASM
-                dma16(srd, off[i], j * step_bytes, lds_addr(buf + 1024 * p));
-#else
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(buf + 1024 * p), 16,
-                                                         off[i], j * step_bytes, 0, 0);
-#endif
-            }
-#endif
+            if (PIECES % NW == 0 || p < PIECES) dma16(srd, off[i], j * step_bytes, lds_addr(buf + 1024 * p));
         }
     };
     // stage the next K/V tiles: issue the DMA early, wait for it late
     auto stage_issue = [&](char *kb_wr, char *vb_wr, int jk, int jv) __attribute__((always_inline)) {
-#if FA_DMA_ASM
-        dma_tile(kr, ksrd, dma_k_off, k_tile_step, kb_wr, jk);
-        dma_tile(vr, vsrd, dma_v_off, v_tile_step, vb_wr, jv);
-#else
-        dma_tile(kr, i32x4{}, dma_k_off, k_tile_step, kb_wr, jk);
-        dma_tile(vr, i32x4{}, dma_v_off, v_tile_step, vb_wr, jv);
-#endif
+        dma_tile(ksrd, dma_k_off, k_tile_step, kb_wr, jk);
+        dma_tile(vsrd, dma_v_off, v_tile_step, vb_wr, jv);
     };
     auto stage_commit = [&]() __attribute__((always_inline)) { vmcnt0(); };
     auto step = [&](auto par_tag, int j) __attribute__((always_inline)) {
@@ -487,11 +473,15 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
         char *kb_wr = smem + (1 - P) * C::TILE_BYTES;
         char *vb_wr = smem + (3 - P) * C::TILE_BYTES;
         stage_issue(kb_wr, vb_wr, j + 1, j + 1);
-        f32x16 s[2];
-        qk(kb_rd, s);
-        typename T::frag pf[2][2];
-        softmax_tile(s, j * C::BN, pf);
-        pv(vb_rd, pf);
+        // causal: a wave whose 32 rows all lie above this key tile would add exactly nothing (every
+        // P = 0, no rescale): it only stages its share of the next tile and meets the barrier
+        if (!CAUSAL || j * C::BN <= qw + 31) {
+            f32x16 s[2];
+            qk(kb_rd, s);
+            typename T::frag pf[2][2];
+            softmax_tile(s, j * C::BN, pf);
+            pv(vb_rd, pf);
+        }
         stage_commit();
         __syncthreads();
     };
