@@ -25,8 +25,13 @@ namespace fa {
 #define FA_BWD_SPLIT_KVL_NC 1   // 1: the non-causal ones too (D=128 non-causal 1.00 -> 0.95 ms)
 #endif
 
-template <int D, bool KVL_ = false>
+template <int D, bool KVL_ = false, bool SKEW_ = false>
 struct BwdSplitCfg {
+    // SKEW (dense, no dropout, dQ by the query-major pass): the P waves run one query tile ahead
+    // of the dS waves, so Q/dO/lse/delta rotate through 3 buffers and P through 2
+    static constexpr bool SKEW = SKEW_;
+    static constexpr int NQB = SKEW ? 3 : 2;
+    static constexpr int NPX = SKEW ? 2 : 1;
     static constexpr int NW = 8;            // waves per workgroup
     static constexpr int NT = 64 * NW;
     static constexpr int KEYW = NW / 2;     // wave pairs, 32 keys each
@@ -37,27 +42,34 @@ struct BwdSplitCfg {
     static constexpr int Q_IMG = BQ * D * 2;
     static constexpr int DS_IMG = BKV * BQ * 2;
     static constexpr int OFF_K = 0;
-    static constexpr int OFF_Q = OFF_K + K_IMG;          // Q[2]
-    static constexpr int OFF_DO = OFF_Q + 2 * Q_IMG;     // dO[2]
-    static constexpr int OFF_DS = OFF_DO + 2 * Q_IMG;
-    static constexpr int OFF_LSE = OFF_DS + DS_IMG;      // lse[2][BQ]
-    static constexpr int OFF_DELTA = OFF_LSE + 2 * BQ * 4;
-    static constexpr int OFF_QLIVE = OFF_DELTA + 2 * BQ * 4;
+    static constexpr int OFF_Q = OFF_K + K_IMG;          // Q[NQB]
+    static constexpr int OFF_DO = OFF_Q + NQB * Q_IMG;   // dO[NQB]
+    static constexpr int OFF_DS = OFF_DO + NQB * Q_IMG;
+    static constexpr int OFF_LSE = OFF_DS + (SKEW ? 0 : DS_IMG);   // lse[NQB][BQ]
+    static constexpr int OFF_DELTA = OFF_LSE + NQB * BQ * 4;
+    static constexpr int OFF_QLIVE = OFF_DELTA + NQB * BQ * 4;
     static constexpr int QLIVE_WORDS = 16;
     // P exchange: per wave pair 4 chunks x 64 lanes x 16 B (chunk-major: conflict-free b128)
     static constexpr int OFF_PX = OFF_QLIVE + QLIVE_WORDS * 8;
     static constexpr int PX_PAIR = 4 * 64 * 16;
     // KVL (causal): K and V rows re-read from LDS images per query tile instead of 32 registers
     static constexpr bool KVL = KVL_;
-    static constexpr int OFF_V = OFF_PX + KEYW * PX_PAIR;
+    static constexpr int OFF_V = OFF_PX + NPX * KEYW * PX_PAIR;
     static constexpr int LDS_BYTES = OFF_V + (KVL ? K_IMG : 0);
     static constexpr int QCH = (BQ * NC + NT - 1) / NT;
 };
 
+#ifndef FA_BWD_SPLIT_SKEW
+#define FA_BWD_SPLIT_SKEW 1   // 1: P waves one query tile ahead of dS waves (dense, no dropout, no dQ)
+#endif
+constexpr bool bwd_split_skew(bool dq, bool dropout, bool sparse) {
+    return FA_BWD_SPLIT_SKEW && !dq && !dropout && !sparse;
+}
+
 // DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
 __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a, const FaBlockMask bm) {
-    using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL>;
+    using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL, bwd_split_skew(DQ, DROPOUT, SPARSE)>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -395,7 +407,100 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
         if (itn < nqt) lds_store_qtile(1 - BUF);
         __syncthreads();
     };
-    if constexpr (SPARSE) {
+    // ---- skewed pipeline (C::SKEW): in step u the P waves take query tile u (S, P -> P image u&1,
+    // dV) while the dS waves take tile u-1 (dZ, dS from P image (u-1)&1, dK). Neither waits for the
+    // other inside a step, so on each SIMD the P wave's exp work runs beside the dS wave's MFMAs and
+    // the other way round; one barrier per step. Tile u+1 is prefetched into Q/dO buffer (u+1)%3.
+    auto sstep = [&](auto qb_tag, int u) __attribute__((always_inline)) {
+        constexpr int QB = decltype(qb_tag)::value;           // buffer of tile u
+        constexpr int QBD = (QB + 2) % 3;                      // buffer of tile u-1 (dS waves)
+        if (u + 1 < nqt) gload_qtile(q_begin + (u + 1) * C::BQ);
+        const int tile = role_p ? u : u - 1;
+        const int q0 = q_begin + tile * C::BQ;
+        const bool has = role_p ? u < nqt : u >= 1;
+        const bool active = has && (!CAUSAL || (q0 + C::BQ - 1 >= kw));
+        char *pxb = px + ((role_p ? u : u - 1) & 1) * (C::KEYW * C::PX_PAIR);
+        if (active) {
+            const char *qimg = smem + C::OFF_Q + (role_p ? QB : QBD) * C::Q_IMG;
+            const char *doimg = smem + C::OFF_DO + (role_p ? QB : QBD) * C::Q_IMG;
+            f32x16 x;
+            const char *aimg = role_p ? qimg : doimg;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) x[r] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < D / 16; ++ks) {
+                const auto qa = as_frag<T>(lds_read128(aimg, S::off(l32, 2 * ks + hi)));
+                if constexpr (C::KVL)
+                    x = T::mfma32(qa, as_frag<T>(lds_read128(role_p ? kimg : smem + C::OFF_V,
+                                                             S::off(32 * kwave + l32, 2 * ks + hi))), x);
+                else
+                    x = T::mfma32(qa, bf[ks], x);
+            }
+            if (role_p) {
+                const float *lse_b = lse_s + QB * C::BQ;
+                const bool need_mask = (q0 + C::BQ > seqlen_q) || (k0 + C::BKV > seqlen_k) || (CAUSAL && q0 < kw + 31);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 lse4 = *reinterpret_cast<const f32x4 *>(lse_b + 8 * g + 4 * hi);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int r = 4 * g + e;
+                        float p = fast_exp2(fmaf(x[r], c_log2, -lse4[e]));
+                        if (need_mask) {
+                            const int q = q0 + crow(r, hi);
+                            if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
+                        }
+                        x[r] = p;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    lds_write128(pxb, j * 1024 + lane * 16,
+                                 u32x4{__float_as_uint(x[4 * j]), __float_as_uint(x[4 * j + 1]),
+                                       __float_as_uint(x[4 * j + 2]), __float_as_uint(x[4 * j + 3])});
+            } else {
+                const float *del_b = del_s + QBD * C::BQ;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const u32x4 pw = lds_read128(pxb, j * 1024 + lane * 16);
+                    const f32x4 del4 = *reinterpret_cast<const f32x4 *>(del_b + 8 * j + 4 * hi);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) x[4 * j + e] = __uint_as_float(pw[e]) * (x[4 * j + e] - del4[e]);
+                }
+            }
+            // dV^T += dO^T P (P waves) or dK^T += Q^T dS (dS waves), A operands by transposed reads
+            const char *timg = role_p ? doimg : qimg;
+#pragma unroll
+            for (int sg = 0; sg < 2; ++sg) {
+                u32x4 pk;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) pk[e] = T::pack2(x[8 * sg + 2 * e], x[8 * sg + 2 * e + 1]);
+                const int rb = 16 * sg + 4 * hi + qq;
+#pragma unroll
+                for (int dt = 0; dt < D / 32; ++dt) {
+                    const int col = 32 * dt + 16 * grp + 4 * pp;
+                    u32x2 a0 = lds_read_tr(timg, S::off8(rb, col));
+                    u32x2 a1 = lds_read_tr(timg, S::off8(rb + 8, col));
+                    acc[dt] = T::mfma32(as_frag<T>(u32x4{a0[0], a0[1], a1[0], a1[1]}), as_frag<T>(pk), acc[dt]);
+                }
+            }
+        }
+        // tile u+1 into buffer (u+1)%3: it held tile u-2, last read by the dS waves in step u-1
+        if (u + 1 < nqt) lds_store_qtile((QB + 1) % 3);
+        __syncthreads();
+    };
+
+    if constexpr (C::SKEW) {
+        // the prologue stored tile 0 in buffer 0; steps u = 0 .. nqt (the last one: dS waves only)
+        int u = 0;
+        for (; u + 2 <= nqt; u += 3) {
+            sstep(std::integral_constant<int, 0>(), u);
+            sstep(std::integral_constant<int, 1>(), u + 1);
+            sstep(std::integral_constant<int, 2>(), u + 2);
+        }
+        if (u <= nqt) sstep(std::integral_constant<int, 0>(), u++);
+        if (u <= nqt) sstep(std::integral_constant<int, 1>(), u++);
+    } else if constexpr (SPARSE) {
         int it = t_first;
         while (it < nqt) {
             int itn = next_qt(it);

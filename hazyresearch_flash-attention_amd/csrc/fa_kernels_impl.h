@@ -59,7 +59,8 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
     if constexpr (D == 128 && FA_BWD_SPLIT128) {
         // dQ either by the split kernel's atomics or by the query-major pass (bwd_dq_direct)
         constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
-        using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL>;
+        using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL,
+                              bwd_split_skew(!DQK, DROPOUT, SPARSE)>;
         auto kern = fa_bwd_split_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
         FA_ENSURE_LDS(kern, C::LDS_BYTES);
         dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
