@@ -251,18 +251,29 @@ def main():
         extra["rotary_qkv_inplace_B8_S2048_H12_D64_bf16"] = {
             "ms": round(ms_r, 4), "GBps": round(rbytes / ms_r / 1e6, 1), "frac_hbm": round(rbytes / ms_r / 1e6 / PEAK_HBM_GBS, 4)}
         # rotary fused into the attention forward (FlashMHA's path: q rotated at the kernel's Q load,
-        # k by a half-size pass) against the separate q+k pass followed by the plain forward
+        # k by a half-size pass) against a separate q+k pass followed by the plain forward. Both legs
+        # read the same pristine qkv (an in-place pass repeated thousands of times drifts the data,
+        # and the softmax's rescale branch makes the kernel time data-dependent): the separate pass
+        # writes rotated q, k to a scratch buffer (same bytes as in place).
+        from flash_attn import flash_attn_hip as hip_
         from flash_attn.flash_attention import FlashAttnRotaryQKVFunc
-        from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func
-        qkv5 = qkv_r.view(8, 2048, 3, 12, 64)
+        from flash_attn.flash_attn_interface import flash_attn_unpadded_func as fa_unp
+        qkv5 = torch.randn(8, 2048, 3, 12, 64, generator=torch.Generator().manual_seed(6)).bfloat16().to(dev)
+        qk_rot = torch.empty(8, 2048, 2, 12, 64, dtype=torch.bfloat16, device=dev)
         cu_r = torch.arange(0, 9 * 2048, 2048, dtype=torch.int32, device=dev)
-        ms_sep, _ = time_events(lambda: flash_attn_unpadded_qkvpacked_func(
-            apply_rotary_emb_qkv_(qkv_r, rc, rs, 12, 64).view(8 * 2048, 3, 12, 64), cu_r, 2048, 0.0), 20, 20)
+        st_x, st_y = (2048 * 3 * 768, 3 * 768, 768, 64), (2048 * 2 * 768, 2 * 768, 768, 64)
+        qr, kr, vr = qk_rot[:, :, 0].view(-1, 12, 64), qk_rot[:, :, 1].view(-1, 12, 64), qkv5[:, :, 2].view(-1, 12, 64)
+
+        def separate():
+            hip_.rotary(qkv5, qk_rot, rc, rs, (8, 2048, 2, 12, 64), st_x, st_y, 2, False)
+            return fa_unp(qr, kr, vr, cu_r, cu_r, 2048, 2048, 0.0)
+
+        ms_sep, _ = time_events(separate, 20, 20)
         ms_fus, _ = time_events(lambda: FlashAttnRotaryQKVFunc.apply(qkv5, rc, rs, 0.0, None, False), 20, 20)
         extra["rotary_attention_fwd_B8_S2048_H12_D64_bf16"] = {
             "separate_pass_ms": round(ms_sep, 4), "fused_q_ms": round(ms_fus, 4),
             "speedup": round(ms_sep / ms_fus, 3)}
-        del qkv_r, qkv5
+        del qkv_r, qkv5, qk_rot
         # C3 forward + backward (the fwd+bwd headline of the reference README charts)
         q3, k3, v3, _, c3q, c3k = make_inputs(8, 12, 2048, 2048, 64, torch.bfloat16, dev)
         q3.requires_grad_(); k3.requires_grad_(); v3.requires_grad_()

@@ -8,8 +8,8 @@
 //     dV = Pd^T dO,  dZ = dO V^T,  delta = rowsum(dO*O),  dS = P * (dZ*M/pk - delta),
 //     dQ = scale * dS K,  dK = scale * dS^T Q.
 //
-// Structure (MI355X-first): grid = (key blocks of 32 NW, H, B); a workgroup = NW waves (8 at
-// D <= 64, 4 at D = 128), one wave owns 32 keys and keeps its dK^T, dV^T accumulators in registers
+// Structure (MI355X-first, D <= 64; D = 128 is fa_bwd_split_kernel.h): grid = (key blocks of
+// 32 NW, H, B); a workgroup = NW = 8 waves, one wave owns 32 keys and keeps its dK^T, dV^T accumulators in registers
 // for the whole kernel; its K, V rows (MFMA B operands) stay in registers too, or, in the causal
 // kernels, are re-read per query tile from LDS images. It sweeps 32-row query tiles: Q and dO tiles are staged into swizzled LDS
 // images that serve both row reads (S = Q K^T, dZ = dO V^T) and transposed reads
@@ -34,23 +34,11 @@ namespace fa {
 #ifndef FA_BWD_KV_LDS
 #define FA_BWD_KV_LDS 1         // 1 (D <= 64, causal): K/V B operands re-read from LDS every query tile
 #endif
-#ifndef FA_BWD_RAWROW
-#define FA_BWD_RAWROW 1         // 1: lse/delta row loads consumed only at the LDS write (no early vmcnt wait)
-#endif
-#ifndef FA_BWD_FULLTILE
-#define FA_BWD_FULLTILE 1       // 1: unguarded dQ atomics on full query tiles
-#endif
-#ifndef FA_BWD_DQ_PREFETCH
-#define FA_BWD_DQ_PREFETCH 1    // 1: dQ MFMA operands read one key step ahead
-#endif
 
 // Waves per workgroup (32 keys each). dQ atomic bytes scale with 1/NW, so both use 8 at D <= 64
 // (causal: 4-wave blocks balanced the triangle better but were slower once K/V moved to LDS).
 template <bool CAUSAL>
 struct BwdWaves { static constexpr int value = CAUSAL ? FA_BWD_CAUSAL_NW : FA_BWD_NONCAUSAL_NW; };
-// D=128: 4 waves (one per SIMD), so each wave may hold 512 registers (VGPR + AGPR)
-template <int D, bool CAUSAL>
-struct BwdWavesD { static constexpr int value = D == 128 ? 4 : BwdWaves<CAUSAL>::value; };
 
 template <int D, int NW_ = 8, bool CAUSAL_ = false>
 struct BwdCfg {
@@ -77,7 +65,6 @@ struct BwdCfg {
     static constexpr bool KV_LDS = FA_BWD_KV_LDS && D <= 64 && CAUSAL_;
     static constexpr int OFF_V = OFF_QLIVE + QLIVE_WORDS * 8;
     static constexpr int LDS_BYTES = OFF_V + (KV_LDS ? K_IMG : 0);
-    static constexpr int QCH = (BQ * NC + NT - 1) / NT;   // staged 16-B chunks per thread per tile
 };
 
 // byte offset in the dS^T image ([key][query], 64-B rows) of query column q (multiple of 4) of
@@ -140,21 +127,19 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
     gstore128((uint16_t *)a.dq + row * a.dq_row_stride + h * a.dq_head_stride + c * 8, w);
 }
 
-#ifndef FA_BWD_BQLOAD
-#define FA_BWD_BQLOAD 1   // 1: query-tile loads through buffer descriptors (32-bit lane offsets)
-#endif
 #ifndef FA_BWD_MINW
 #define FA_BWD_MINW 2   // __launch_bounds__ minimum waves per SIMD (2: two workgroups per CU when causal)
 #endif
 #if FA_BWD_MINW > 0
-#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWavesD<D, C>::value), (D == 128 ? 1 : FA_BWD_MINW))
+#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWaves<C>::value), FA_BWD_MINW)
 #else
-#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWavesD<D, C>::value))
+#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWaves<C>::value))
 #endif
 // DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
 __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaBlockMask bm) {
-    using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value, CAUSAL>;
+    static_assert(D <= 64, "D = 128 takes fa_bwd_split_kernel");
+    using C = BwdCfg<D, BwdWaves<CAUSAL>::value, CAUSAL>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -246,69 +231,50 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     const int q_begin = CAUSAL ? k0 : 0;   // rows q < k0 see no key of this block
     const int nqt = seqlen_q > q_begin ? (seqlen_q - q_begin + C::BQ - 1) / C::BQ : 0;
 
-    // ---- query-tile staging: issue the next tile's loads early, write them late (T14), into
-    // the other half of the double-buffered Q/dO/lse/delta images.
-    u32x4 qst[C::QCH], dst[C::QCH];
+    // ---- query-tile staging (T14): a tile is loaded into registers two steps before its use and
+    // written to its LDS image one step before. The two halves of the workgroup take turns: half
+    // g = tid / (NT/2) stages the tiles of step parity g (thread l of the half: the Q and dO
+    // chunk l, and for l < BQ the lse and delta of row l), so each thread holds one tile's
+    // registers, and the wait at a tile's LDS write no longer covers the dQ atomics of the step
+    // that issued its loads. Loads are buffer loads (lane offset + scalar tile offset; the
+    // descriptors end at row seqlen_q, so rows past it read as zeros).
+    constexpr int CH = C::BQ * C::NC;
+    constexpr int HALF = C::NT / 2;
+    static_assert(CH <= HALF && HALF % 64 == 0, "one Q and one dO chunk per thread of a half");
+    const int stg_half = tid >= HALF;             // wave-uniform
+    const int sl = tid - HALF * stg_half;
+    const int crow_ = sl / C::NC, ccol = sl % C::NC;
+    const bool chunk_ok = sl < CH && ccol * 8 < head_dim;
+    u32x4 qst = {0u, 0u, 0u, 0u}, dst = {0u, 0u, 0u, 0u};
     float lse_st = 0.f, del_st = 0.f;
-    // BQLOAD: Q/dO tile loads as buffer loads, lane offset + scalar tile offset; the descriptors end
-    // at row seqlen_q, so rows past it read as zeros (32-bit lane offsets instead of 64-bit addresses)
     const auto q_rs = make_rsrc_n(qp, seqlen_q * (int)a.q_row_stride * 2);
     const auto do_rs = make_rsrc_n(dop, seqlen_q * (int)a.do_row_stride * 2);
-    int qld_off[C::QCH], dold_off[C::QCH];
-#pragma unroll
-    for (int i = 0; i < C::QCH; ++i) {
-        const int idx = tid + C::NT * i;
-        const int row = idx / C::NC, c = idx % C::NC;
-        const bool okc = idx < C::BQ * C::NC && c * 8 < head_dim;
-        qld_off[i] = okc ? (row * (int)a.q_row_stride + c * 8) * 2 : OOB;
-        dold_off[i] = okc ? (row * (int)a.do_row_stride + c * 8) * 2 : OOB;
-    }
+    const int qld_off = chunk_ok ? (crow_ * (int)a.q_row_stride + ccol * 8) * 2 : OOB;
+    const int dold_off = chunk_ok ? (crow_ * (int)a.do_row_stride + ccol * 8) * 2 : OOB;
+    const int st_off = S::off(crow_, ccol);
     auto gload_qtile = [&](int q0n) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < C::QCH; ++i) {
-            if (FA_BWD_BQLOAD) {
-                qst[i] = bload128s(q_rs, qld_off[i], q0n * (int)a.q_row_stride * 2);
-                dst[i] = bload128s(do_rs, dold_off[i], q0n * (int)a.do_row_stride * 2);
-            } else {
-                const int idx = tid + C::NT * i;
-                const int row = idx / C::NC, c = idx % C::NC;
-                const int q = q0n + row;
-                const u32x4 z = {0u, 0u, 0u, 0u};
-                const bool ok = idx < C::BQ * C::NC && q < seqlen_q && c * 8 < head_dim;
-                qst[i] = ok ? gload128(qp + (int64_t)q * a.q_row_stride + c * 8) : z;
-                dst[i] = ok ? gload128(dop + (int64_t)q * a.do_row_stride + c * 8) : z;
-            }
+        if (sl < CH) {
+            qst = bload128s(q_rs, qld_off, q0n * (int)a.q_row_stride * 2);
+            dst = bload128s(do_rs, dold_off, q0n * (int)a.do_row_stride * 2);
         }
-        if (tid < C::BQ) {
-            const int q = q0n + tid;
-            if (FA_BWD_RAWROW) {
-                // unconditional loads of a clamped row, used only at the LDS write: no wait on
-                // them (and on the tile loads issued before them) at the top of the step. Rows
-                // past seqlen_q are masked to P = 0 whatever their constants.
-                const int qc = min(q, seqlen_q - 1);
-                lse_st = lse_g[qc];
-                del_st = del_g[qc];
-            } else {
-                lse_st = q < seqlen_q ? lse_g[q] * LOG2E : 0.f;
-                del_st = q < seqlen_q ? del_g[q] : 0.f;
-            }
+        // unconditional loads of a clamped row, used only at the LDS write (rows past seqlen_q
+        // are masked to P = 0 whatever their constants)
+        if (sl < C::BQ) {
+            const int qc = min(q0n + sl, seqlen_q - 1);
+            lse_st = lse_g[qc];
+            del_st = del_g[qc];
         }
     };
     auto lds_store_qtile = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < C::QCH; ++i) {
-            const int idx = tid + C::NT * i;
-            if ((C::BQ * C::NC) % C::NT == 0 || idx < C::BQ * C::NC) {
-                const int row = idx / C::NC, c = idx % C::NC;
-                lds_write128(smem + C::OFF_Q + buf * C::Q_IMG, S::off(row, c), qst[i]);
-                lds_write128(smem + C::OFF_DO + buf * C::Q_IMG, S::off(row, c), dst[i]);
-            }
+        if (sl < CH) {
+            lds_write128(smem + C::OFF_Q + buf * C::Q_IMG, st_off, qst);
+            lds_write128(smem + C::OFF_DO + buf * C::Q_IMG, st_off, dst);
         }
-        if (tid < C::BQ) {
+        if (sl < C::BQ) {
             // one lane offset for both rows' constants (the image offsets fold into the
             // instruction), so no per-buffer address stays live across the loop
-            lds_write32(smem + C::OFF_LSE + buf * C::BQ * 4, 4 * tid, FA_BWD_RAWROW ? lse_st * LOG2E : lse_st);
-            lds_write32(smem + C::OFF_DELTA + buf * C::BQ * 4, 4 * tid, del_st);
+            lds_write32(smem + C::OFF_LSE + buf * C::BQ * 4, 4 * sl, lse_st * LOG2E);
+            lds_write32(smem + C::OFF_DELTA + buf * C::BQ * 4, 4 * sl, del_st);
         }
     };
     // ---- block sparsity (fa_bwd_block): this workgroup's keys lie in one 256-key column block
@@ -345,21 +311,31 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             return nqt;
         }
     };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
     const int t_first = SPARSE ? next_qt(-1) : 0;
+    const int t_second = t_first < nqt ? next_qt(t_first) : nqt;
     if (t_first < nqt) {
-        gload_qtile(q_begin + t_first * C::BQ);
-        lds_store_qtile(0);
+        if (stg_half == 0) {
+            gload_qtile(q_begin + t_first * C::BQ);
+            lds_store_qtile(0);
+        } else if (t_second < nqt) {
+            gload_qtile(q_begin + t_second * C::BQ);
+        }
     }
     __syncthreads();
 
-    auto qstep = [&](auto par_tag, int it, int itn) __attribute__((always_inline)) {
+    // step of tile `it` (LDS buffer BUF); itn, itnn: the next two live tiles (nqt if none)
+    auto qstep = [&](auto par_tag, int it, int itn, int itnn) __attribute__((always_inline)) {
         constexpr int BUF = decltype(par_tag)::value;
+        // half BUF loads tile itnn now; half 1-BUF writes tile itn (loaded a step ago) to LDS
+        const bool my_load = stg_half == BUF, my_store = stg_half != BUF;
         char *qimg = smem + C::OFF_Q + BUF * C::Q_IMG;
         char *doimg = smem + C::OFF_DO + BUF * C::Q_IMG;
         const float *lse_b = lse_s + BUF * C::BQ;
         const float *del_b = del_s + BUF * C::BQ;
         const int q0 = q_begin + it * C::BQ;
-        if (itn < nqt) gload_qtile(q_begin + itn * C::BQ);
+        if (my_load && itnn < nqt) gload_qtile(q_begin + itnn * C::BQ);
         // block sparsity: a dead 16-row half of a live tile is masked (P = 0 there)
         const bool dead0 = SPARSE && !row_live(q0 >> 4);
         const bool dead1 = SPARSE && !row_live((q0 >> 4) + 1);
@@ -483,31 +459,22 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                         u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
                         bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
                     };
-                    if constexpr (FA_BWD_DQ_PREFETCH) {
-                        // operands of key step ks+1 are read before the MFMA of step ks
-                        u32x4 av, bv, avn, bvn;
-                        dq_operands(0, av, bv);
+                    // operands of key step ks+1 are read before the MFMA of step ks
+                    u32x4 av, bv, avn, bvn;
+                    dq_operands(0, av, bv);
     #pragma unroll
-                        for (int ks = 0; ks < C::BKV / 32; ++ks) {
-                            if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
-                            acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
-                            av = avn;
-                            bv = bvn;
-                        }
-                    } else {
-    #pragma unroll
-                        for (int ks = 0; ks < C::BKV / 32; ++ks) {
-                            u32x4 av, bv;
-                            dq_operands(ks, av, bv);
-                            acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
-                        }
+                    for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                        if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
+                        acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
+                        av = avn;
+                        bv = bvn;
                     }
                     const int d = dbase + (lane & 15);
                     // the prefetched query tile goes to LDS first: its vmcnt wait then covers only
                     // loads (vmcnt retires in issue order), and these atomics have a whole tile of
                     // compute before the next wait
-                    if (t0 == 0 && itn < nqt) lds_store_qtile(1 - BUF);
-                    if (FA_BWD_FULLTILE && q0 + C::BQ <= seqlen_q && head_dim == D) {
+                    if (t0 == 0 && my_store && itn < nqt) lds_store_qtile(1 - BUF);
+                    if (q0 + C::BQ <= seqlen_q && head_dim == D) {
                         // full tile (wave-uniform test): the four atomics without per-lane guards
                         float *base = dqa + (int64_t)(q0 + 16 * qh + 4 * g4) * dqa_row + d;
     #pragma unroll
@@ -523,24 +490,26 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             }
         }
         // waves without a dQ tile (or kernels without dQ) store the prefetched tile here
-        if (itn < nqt && (!DQ || wave >= 2 * (D / 16))) lds_store_qtile(1 - BUF);
+        if (my_store && itn < nqt && (!DQ || wave >= 2 * (D / 16))) lds_store_qtile(1 - BUF);
         __syncthreads();
     };
     if constexpr (SPARSE) {
-        int it = t_first;
+        int it = t_first, itn = t_second;
         while (it < nqt) {
-            int itn = next_qt(it);
-            qstep(std::integral_constant<int, 0>(), it, itn);
+            int itnn = itn < nqt ? next_qt(itn) : nqt;
+            qstep(I0(), it, itn, itnn);
             it = itn;
+            itn = itnn;
             if (it >= nqt) break;
-            itn = next_qt(it);
-            qstep(std::integral_constant<int, 1>(), it, itn);
+            itnn = itn < nqt ? next_qt(itn) : nqt;
+            qstep(I1(), it, itn, itnn);
             it = itn;
+            itn = itnn;
         }
     } else {
         for (int it = 0; it < nqt; it += 2) {
-            qstep(std::integral_constant<int, 0>(), it, it + 1);
-            if (it + 1 < nqt) qstep(std::integral_constant<int, 1>(), it + 1, it + 2);
+            qstep(I0(), it, it + 1, it + 2);
+            if (it + 1 < nqt) qstep(I1(), it + 1, it + 2, it + 3);
         }
     }
 

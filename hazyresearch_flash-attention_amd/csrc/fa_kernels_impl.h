@@ -56,8 +56,9 @@ static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStr
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE>
 static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
-    if constexpr (D == 128 && FA_BWD_SPLIT128) {
-        // dQ either by the split kernel's atomics or by the query-major pass (bwd_dq_direct)
+    // D = 128: the P / dS wave split (fa_bwd_split_kernel.h); D <= 64: fa_bwd_kernel. dQ either by
+    // the main kernel's atomics or by the query-major pass (bwd_dq_direct)
+    if constexpr (D == 128) {
         constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
         using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL,
                               bwd_split_skew(!DQK, DROPOUT, SPARSE)>;
@@ -74,22 +75,23 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
             hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a);
         }
         return hipGetLastError();
+    } else {
+        using C = BwdCfg<D, BwdWaves<CAUSAL>::value, CAUSAL>;
+        constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
+        auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
+        FA_ENSURE_LDS(kern, C::LDS_BYTES);
+        dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
+        hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
+        if constexpr (DQK) {
+            constexpr int NWQ = FA_BWD_DQ_NW;
+            using CQ = DqCfg<D, NWQ>;
+            auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
+            FA_ENSURE_LDS(kq, CQ::LDS_BYTES);
+            dim3 gq((a.max_seqlen_q + CQ::BM - 1) / CQ::BM, a.nheads, a.batch);
+            hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a);
+        }
+        return hipGetLastError();
     }
-    using C = BwdCfg<D, BwdWavesD<D, CAUSAL>::value, CAUSAL>;
-    constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
-    auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
-    FA_ENSURE_LDS(kern, C::LDS_BYTES);
-    dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
-    if constexpr (DQK) {
-        constexpr int NWQ = FA_BWD_DQ_NW;
-        using CQ = DqCfg<D, NWQ>;
-        auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
-        FA_ENSURE_LDS(kq, CQ::LDS_BYTES);
-        dim3 gq((a.max_seqlen_q + CQ::BM - 1) / CQ::BM, a.nheads, a.batch);
-        hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a);
-    }
-    return hipGetLastError();
 }
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT>

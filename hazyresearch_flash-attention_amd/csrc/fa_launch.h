@@ -21,9 +21,6 @@ hipError_t launch_scatter_add_rows(const void *src, int64_t src_stride, const in
 hipError_t launch_rotary(const FaRotaryArgs &a, hipStream_t s);
 hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t stream);
 
-#ifndef FA_BWD_SPLIT128
-#define FA_BWD_SPLIT128 1   // 1: D = 128 backward with the P / dS wave split (fa_bwd_split_kernel.h)
-#endif
 #ifndef FA_BWD_DQK
 #define FA_BWD_DQK 1        // 1: D = 128 dense, no dropout: dQ by the query-major fa_bwd_dq_kernel
 #endif
@@ -31,7 +28,7 @@ hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t stream);
 #ifndef FA_BWD_DQK_MIN_D
 #define FA_BWD_DQK_MIN_D 128   // smallest head-dim tile that takes the query-major dQ pass
 #endif
-constexpr bool bwd_dqk_tile(int D) { return FA_BWD_DQK && D >= FA_BWD_DQK_MIN_D && (D < 128 || FA_BWD_SPLIT128); }
+constexpr bool bwd_dqk_tile(int D) { return FA_BWD_DQK && D >= FA_BWD_DQK_MIN_D; }
 inline bool bwd_dq_direct(const FaBwdArgs &a, const FaBlockMask &bm) {
     const int tile = a.head_dim <= 32 ? 32 : a.head_dim <= 64 ? 64 : 128;
     return bwd_dqk_tile(tile) && a.p_dropout == 0.f && bm.mask == nullptr && a.max_seqlen_k > 0;

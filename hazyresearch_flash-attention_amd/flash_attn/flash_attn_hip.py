@@ -177,7 +177,10 @@ def _packer(cls):
         o = getattr(cls, name).offset
         if o > off:
             fmt += f"{o - off}x"
-        fmt += codes[typ]
+        if issubclass(typ, ctypes.Array):
+            fmt += f"{typ._length_}{codes[typ._type_]}"
+        else:
+            fmt += codes[typ]
         off = o + ctypes.sizeof(typ)
     if ctypes.sizeof(cls) > off:
         fmt += f"{ctypes.sizeof(cls) - off}x"
@@ -186,35 +189,34 @@ def _packer(cls):
     return st
 
 
-_fwd_packer = None
+_packers = {}
 
 
-def _fwd_call():
-    """(packer, per-thread argument buffer, its address, raw fa_fwd taking the address)."""
-    global _fwd_packer
-    c = getattr(_tls, "fwd_raw", None)
+def _raw_call(cls, symbol, nargs=2):
+    """(packer, per-thread argument buffer, its address, raw `symbol` taking the address and
+    nargs-1 further pointers) for the argument struct `cls`."""
+    key = (cls, symbol)
+    c = getattr(_tls, "raw", {}).get(key)
     if c is None:
-        if _fwd_packer is None:
-            _fwd_packer = _packer(FaFwdArgs)
-        buf = ctypes.create_string_buffer(_fwd_packer.size)
-        fn = lib()["fa_fwd"]            # a second prototype of the same symbol, taking the address
-        fn.argtypes = [_vp, _vp]
+        st = _packers.get(cls)
+        if st is None:
+            st = _packers[cls] = _packer(cls)
+        buf = ctypes.create_string_buffer(st.size)
+        fn = lib()[symbol]              # a second prototype of the same symbol, taking the address
+        fn.argtypes = [_vp] * nargs
         fn.restype = ctypes.c_int
-        c = (_fwd_packer, buf, ctypes.addressof(buf), fn)
-        _tls.fwd_raw = c
+        c = (st, buf, ctypes.addressof(buf), fn)
+        if not hasattr(_tls, "raw"):
+            _tls.raw = {}
+        _tls.raw[key] = c
     return c
 
 
+def _fwd_call():
+    return _raw_call(FaFwdArgs, "fa_fwd")
+
+
 _tls = threading.local()
-
-
-def _args(kind):
-    # one reusable ctypes struct per host thread: the C side copies it at launch
-    a = getattr(_tls, kind, None)
-    if a is None:
-        a = FaFwdArgs() if kind == "fwd" else FaBwdArgs()
-        setattr(_tls, kind, a)
-    return a
 
 
 def _on_device(dev):
@@ -458,34 +460,28 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
             seed, offset, offset_dev = _unpack_rng(rng_state if rng_state is not None else reserve_rng(dev, gen))
         else:
             seed, offset, offset_dev = 0, 0, None
-        a = _args("bwd")
-        a.dout, a.q, a.k, a.v, a.out = dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
-        a.softmax_lse = softmax_lse.data_ptr()
-        a.dq, a.dk, a.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
-        a.softmax_d = softmax_d.data_ptr()
-        a.dq_accum = dq_accum.data_ptr() if dq_accum is not None else None
-        a.cu_seqlens_q, a.cu_seqlens_k = cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr()
-        a.do_row_stride, a.do_head_stride = dout.stride(0), dout.stride(1)
-        a.q_row_stride, a.q_head_stride = q.stride(0), q.stride(1)
-        a.k_row_stride, a.k_head_stride = k.stride(0), k.stride(1)
-        a.v_row_stride, a.v_head_stride = v.stride(0), v.stride(1)
-        a.o_row_stride, a.o_head_stride = out.stride(0), out.stride(1)
-        a.dq_row_stride, a.dq_head_stride = dq.stride(0), dq.stride(1)
-        a.dk_row_stride, a.dk_head_stride = dk.stride(0), dk.stride(1)
-        a.dv_row_stride, a.dv_head_stride = dv.stride(0), dv.stride(1)
-        a.batch, a.nheads, a.head_dim = batch, nheads, head_dim
-        a.max_seqlen_q, a.max_seqlen_k = int(max_seqlen_q), int(max_seqlen_k)
-        a.total_q, a.lse_stride = total_q, lse_stride
-        a.softmax_scale = float(softmax_scale)
-        a.p_dropout = float(p_dropout)
-        a.rng_seed, a.rng_offset, a.rng_offset_dev = seed, offset, offset_dev
-        a.is_causal = 1 if is_causal else 0
-        a.dtype = dt
+        # FaBwdArgs field order (include/fa_hip.h), packed in one call
         if layout is None:
-            rc = lib().fa_bwd(ctypes.byref(a), _stream_ptr(dev))
+            packer, buf, addr, raw_bwd = _raw_call(FaBwdArgs, "fa_bwd")
+        else:
+            packer, buf, addr, raw_bwd = _raw_call(FaBwdArgs, "fa_bwd_block", 3)
+        dos, qs, ks, vs, os_ = dout.stride(), q.stride(), k.stride(), v.stride(), out.stride()
+        dqs, dks, dvs = dq.stride(), dk.stride(), dv.stride()
+        packer.pack_into(
+            buf, 0, dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(),
+            softmax_lse.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), softmax_d.data_ptr(),
+            dq_accum.data_ptr() if dq_accum is not None else 0,
+            cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr(),
+            dos[0], dos[1], qs[0], qs[1], ks[0], ks[1], vs[0], vs[1], os_[0], os_[1],
+            dqs[0], dqs[1], dks[0], dks[1], dvs[0], dvs[1],
+            batch, nheads, head_dim, int(max_seqlen_q), int(max_seqlen_k), total_q, lse_stride,
+            float(softmax_scale), float(p_dropout), seed, offset, offset_dev or 0,
+            1 if is_causal else 0, dt)
+        if layout is None:
+            rc = raw_bwd(addr, _stream_ptr(dev))
         else:
             m, _keep = _mask_struct(layout, dev)
-            rc = lib().fa_bwd_block(ctypes.byref(a), ctypes.byref(m), _stream_ptr(dev))
+            rc = raw_bwd(addr, ctypes.addressof(m), _stream_ptr(dev))
         if rc != 0:
             _raise(rc, "fa_bwd")
     return softmax_d
@@ -532,19 +528,14 @@ def rotary(x, y, cos, sin, shape, x_strides, y_strides, nrot, inverse):
     """fa_rotary over the (B, S, NSLOT, H, D) views of x and y given by `shape` and element
     strides (batch, seq, slot, head); y may be x (in place)."""
     B, S, NS, H, D = shape
-    a = FaRotaryArgs()
-    a.x, a.y = x.data_ptr(), y.data_ptr()
-    a.cos, a.sin = cos.data_ptr(), sin.data_ptr()
-    for i in range(4):
-        a.x_strides[i] = int(x_strides[i])
-        a.y_strides[i] = int(y_strides[i])
-    a.table_stride = cos.stride(0)
-    a.batch, a.seqlen, a.nslot, a.nheads, a.head_dim = B, S, NS, H, D
-    a.nrot, a.inverse = nrot, 1 if inverse else 0
-    a.dtype = _dtype_code(x.dtype)
     _check(cos.stride(0) == sin.stride(0), "cos and sin tables must share a row stride")
+    packer, buf, addr, raw = _raw_call(FaRotaryArgs, "fa_rotary")
+    xs, ys = x_strides, y_strides
+    packer.pack_into(buf, 0, x.data_ptr(), y.data_ptr(), cos.data_ptr(), sin.data_ptr(),
+                     int(xs[0]), int(xs[1]), int(xs[2]), int(xs[3]), int(ys[0]), int(ys[1]), int(ys[2]), int(ys[3]),
+                     cos.stride(0), B, S, NS, H, D, nrot, 1 if inverse else 0, _dtype_code(x.dtype))
     with _on_device(x.device):
-        rc = lib().fa_rotary(ctypes.byref(a), _stream_ptr(x.device))
+        rc = raw(addr, _stream_ptr(x.device))
     if rc != 0:
         _raise(rc, "fa_rotary")
     return y

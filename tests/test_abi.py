@@ -189,27 +189,38 @@ def test_bert_padding_host_path_matches_reference_semantics():
     assert torch.equal(x.grad.reshape(21, 4)[idx], torch.full((15, 4), 3.0))
 
 
-def test_fwd_packer_matches_ctypes_layout():
-    """The one-call struct.pack_into image of FaFwdArgs (flash_attn_hip._fwd_call) is byte-identical
-    to the ctypes mirror filled field by field (whose size fa_query checks against the C header)."""
+@pytest.mark.parametrize("cls_name", ["FaFwdArgs", "FaBwdArgs", "FaRotaryArgs"])
+def test_packer_matches_ctypes_layout(cls_name):
+    """The one-call struct.pack_into image of an argument struct (flash_attn_hip._raw_call) is
+    byte-identical to the ctypes mirror filled field by field (whose size fa_query checks against
+    the C header)."""
     import random
     from flash_attn import flash_attn_hip as hip
-    packer = hip._packer(hip.FaFwdArgs)
+    cls = getattr(hip, cls_name)
+    packer = hip._packer(cls)
     rnd = random.Random(1)
-    a = hip.FaFwdArgs()
-    vals = []
-    for name, typ in hip.FaFwdArgs._fields_:
+    a = cls()
+
+    def draw(typ):
         if typ is ctypes.c_float:
-            v = rnd.random()
-            v = ctypes.c_float(v).value
-        elif typ is ctypes.c_int32:
-            v = rnd.randint(-2 ** 31, 2 ** 31 - 1)
-        elif typ is ctypes.c_int64:
-            v = rnd.randint(-2 ** 63, 2 ** 63 - 1)
+            return ctypes.c_float(rnd.random()).value
+        if typ is ctypes.c_int32:
+            return rnd.randint(-2 ** 31, 2 ** 31 - 1)
+        if typ is ctypes.c_int64:
+            return rnd.randint(-2 ** 63, 2 ** 63 - 1)
+        return rnd.randint(0, 2 ** 64 - 1)
+
+    vals = []
+    for name, typ in cls._fields_:
+        if issubclass(typ, ctypes.Array):
+            arr = getattr(a, name)
+            for i in range(typ._length_):
+                arr[i] = draw(typ._type_)
+                vals.append(arr[i])
         else:
-            v = rnd.randint(0, 2 ** 64 - 1)
-        setattr(a, name, v)
-        vals.append(v)
+            v = draw(typ)
+            setattr(a, name, v)
+            vals.append(v)
     buf = ctypes.create_string_buffer(packer.size)
     packer.pack_into(buf, 0, *vals)
     assert bytes(buf) == bytes(a)

@@ -23,7 +23,7 @@ import torch  # noqa: E402
 
 from flash_attn import flash_attn_hip as hip  # noqa: E402
 from flash_attn.flash_attention import FlashAttnRotaryQKVFunc  # noqa: E402
-from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func  # noqa: E402
+from flash_attn.flash_attn_interface import flash_attn_unpadded_func, flash_attn_unpadded_qkvpacked_func  # noqa: E402
 from flash_attn.rotary import apply_rotary_emb_qkv_  # noqa: E402
 from oracle.rotary_ref import rotary_tables  # noqa: E402
 
@@ -56,11 +56,16 @@ def main():
     qkv = torch.randn(B, S, 3, H, D, generator=g).bfloat16().cuda()
     cos, sin = (t.cuda() for t in rotary_tables(S, D, torch.bfloat16))
     cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device="cuda")
-    work = qkv.clone()
+    # the separate leg writes rotated q, k to a scratch buffer (same bytes as in place) so both
+    # legs attend over the same data: a pass repeated in place drifts it, and the kernel's
+    # rescale branch makes its time data-dependent
+    qk_rot = torch.empty(B, S, 2, H, D, dtype=qkv.dtype, device="cuda")
+    st_x, st_y = (S * 3 * H * D, 3 * H * D, H * D, D), (S * 2 * H * D, 2 * H * D, H * D, D)
+    qr, kr, vr = qk_rot[:, :, 0].view(-1, H, D), qk_rot[:, :, 1].view(-1, H, D), qkv[:, :, 2].view(-1, H, D)
 
     def separate():
-        w = apply_rotary_emb_qkv_(work, cos, sin)
-        return flash_attn_unpadded_qkvpacked_func(w.view(B * S, 3, H, D), cu, S, 0.0)
+        hip.rotary(qkv, qk_rot, cos, sin, (B, S, 2, H, D), st_x, st_y, 2, False)
+        return flash_attn_unpadded_func(qr, kr, vr, cu, cu, S, S, 0.0)
 
     def fused_q():
         return FlashAttnRotaryQKVFunc.apply(qkv, cos, sin, 0.0, None, False)
@@ -73,6 +78,7 @@ def main():
     ref = flash_attn_unpadded_qkvpacked_func(apply_rotary_emb_qkv_(qkv.clone(), cos, sin).view(B * S, 3, H, D),
                                              cu, S, 0.0)
     res["fused_q_bitexact"] = bool(torch.equal(fused_q().reshape(B * S, H, D), ref))
+    res["separate_bitexact"] = bool(torch.equal(separate(), ref))
     var = os.path.join(ROOT, "hazyresearch_flash-attention_amd", "build", "var_rotk.so")
     if os.path.exists(var):
         L = ctypes.CDLL(var)
