@@ -30,18 +30,26 @@ static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipSt
 #define FA_FWD_NW_DEFAULT 8
 #endif
 // Waves per workgroup. 8 (256 query rows, two workgroups per CU at 128 registers) measured
-// fastest without dropout on every BASELINE config, including the short S=512 one (428 vs 420
-// TF/s for 8/4). With dropout the kernel needs ~168 registers: 8-wave workgroups then fit one per
-// CU (two waves per SIMD), 4-wave ones three per CU, and C3's forward runs 457 vs 369 TF/s.
-// FA_FWD_NW=2|4|8 overrides the choice for tuning.
+// fastest without dropout on the BASELINE configs, except when the 8-wave grid fills less than
+// two rounds of CU slots unevenly (fewer than 2 * CUs workgroups, not a multiple of the CU
+// count): some CUs would then run two workgroups and others one, and 4-wave workgroups (four
+// per CU) spread the same rows evenly. B4 H12 S2048 D64 (384 workgroups): 793 vs 728 TF/s; C5
+// (256 = one per CU) and C2 (192) keep 8 (808 vs 842, 424 vs 431). With dropout the kernel
+// needs ~168 registers: 8-wave workgroups then fit one per CU (two waves per SIMD), 4-wave
+// ones three per CU, and C3's forward runs 457 vs 369 TF/s. FA_FWD_NW=2|4|8 overrides the
+// choice for tuning.
 template <int D, bool DROPOUT>
-static int pick_fwd_waves(const FaFwdArgs &) {
+static int pick_fwd_waves(const FaFwdArgs &a) {
     static const int forced = [] {
         const char *e = getenv("FA_FWD_NW");
         return e ? atoi(e) : 0;
     }();
     if (forced == 2 || forced == 4 || forced == 8) return forced;
-    return DROPOUT && D <= 64 ? 4 : FA_FWD_NW_DEFAULT;
+    if (DROPOUT && D <= 64) return 4;
+    const int64_t nwg8 = (int64_t)((a.max_seqlen_q + 255) / 256) * a.nheads * a.batch;
+    const int cus = device_cus();
+    if (cus > 0 && nwg8 > cus && nwg8 < 2 * cus && nwg8 % cus != 0) return 4;
+    return FA_FWD_NW_DEFAULT;
 }
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT>

@@ -49,6 +49,20 @@ static hipError_t ensure_lds(std::atomic<uint64_t> &done, K kern, int lds) {
     if (e == hipSuccess) done.fetch_or(bit, std::memory_order_release);
     return e;
 }
+// Compute units of the current device (cached per device; 0 if unknown).
+static inline int device_cus() {
+    static std::atomic<int> cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (dev < 64) {
+        const int c = cus[dev].load(std::memory_order_relaxed);
+        if (c) return c;
+    }
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (dev < 64) cus[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
 #define FA_ENSURE_LDS(kern, lds)                                   \
     do {                                                           \
         static std::atomic<uint64_t> fa_lds_done_{0};              \

@@ -41,3 +41,10 @@ def test_long_context_s16384_d64_causal():
 def test_long_context_s8192_d64_dropout_fp16():
     """S=8192 fp16 causal with dropout (atomic-dQ D=64 backward over 32 key blocks)."""
     run_case("separate", 1, 8192, 8192, 2, 64, torch.float16, True, 0.1, mode="full")
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_forward_grid_balance_four_wave_workgroups(causal):
+    """B=1 H=36 S=2048: 288 eight-wave workgroups, between one and two per CU of a 256-CU device,
+    so the launcher picks 4-wave workgroups (fa_kernels_impl.h pick_fwd_waves) without dropout."""
+    run_case("separate", 1, 2048, 2048, 36, 64, torch.bfloat16, causal, 0.0)
