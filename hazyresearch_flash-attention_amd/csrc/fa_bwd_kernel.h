@@ -15,9 +15,10 @@
 // images that serve both row reads (S = Q K^T, dZ = dO V^T) and transposed reads
 // (dV^T += dO^T Pd, dK^T += Q^T dS). Scores are computed with the key on the MFMA lane, so
 // P/dS accumulators are already the B operands of dV^T/dK^T. dS crosses LDS once (a [key][query]
-// image) for dQ = dS K, computed with 16x16x32 MFMAs so each wave owns whole dQ tiles summed
-// over all the block's keys, then added with fp32 atomics into a workspace; a last kernel scales
-// and converts dQ into the (possibly strided) output.
+// image, double-buffered) for dQ = dS K, computed one query tile later (so a step needs one
+// barrier) with 16x16x32 MFMAs, each wave owning whole dQ tiles summed over all the block's keys,
+// then added with fp32 atomics into a workspace; a last kernel scales and converts dQ into the
+// (possibly strided) output.
 #pragma once
 
 #include "fa_common.h"
@@ -54,7 +55,7 @@ struct BwdCfg {
     static constexpr int OFF_Q = OFF_K + K_IMG;          // Q[2]  (double-buffered query tiles)
     static constexpr int OFF_DO = OFF_Q + 2 * Q_IMG;     // dO[2]
     static constexpr int OFF_DS = OFF_DO + 2 * Q_IMG;
-    static constexpr int OFF_LSE = OFF_DS + DS_IMG;      // lse[2][BQ]
+    static constexpr int OFF_LSE = OFF_DS + 2 * DS_IMG;  // dS[2] (dQ runs one tile behind); lse[2][BQ]
     static constexpr int OFF_DELTA = OFF_LSE + 2 * BQ * 4;
     static constexpr int OFF_QLIVE = OFF_DELTA + 2 * BQ * 4;   // block-sparse: live query tiles, 1 bit each
     static constexpr int QLIVE_WORDS = 16;                      // <= 1024 tiles (32768 rows)
@@ -325,8 +326,62 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     }
     __syncthreads();
 
-    // step of tile `it` (LDS buffer BUF); itn, itnn: the next two live tiles (nqt if none)
-    auto qstep = [&](auto par_tag, int it, int itn, int itnn) __attribute__((always_inline)) {
+    // ---- dQ[q][d] += dS[q][key] K[key][d] over the BKV keys (16x16x32 MFMAs) of the query tile
+    // at row qd, from the dS image dsr; the 2*(D/16) output tiles of 16 query rows x 16 columns
+    // are dealt round-robin to the waves, each summing over every key of the block, so one fp32
+    // atomic per element per block. store_buf >= 0: the waves holding a dQ tile write the staged
+    // query tile into LDS buffer store_buf before their atomics.
+    auto dq_phase = [&](const char *dsr, int qd, int store_buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t0 = 0; t0 < 2 * (D / 16); t0 += C::NW) {
+            const int t = t0 + wave;
+            if (t < 2 * (D / 16)) {
+                const int qh = t & 1;
+                const int dbase = 16 * (t >> 1);
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                auto dq_operands = [&](int ks, u32x4 &av, u32x4 &bv) __attribute__((always_inline)) {
+                    const int r0 = 32 * ks + 8 * g4 + qq;
+                    u32x2 a0 = lds_read_tr(dsr, ds_off(r0, 16 * qh + 4 * pp));
+                    u32x2 a1 = lds_read_tr(dsr, ds_off(r0 + 4, 16 * qh + 4 * pp));
+                    av = u32x4{a0[0], a0[1], a1[0], a1[1]};
+                    u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
+                    u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
+                    bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
+                };
+                // operands of key step ks+1 are read before the MFMA of step ks
+                u32x4 av, bv, avn, bvn;
+                dq_operands(0, av, bv);
+#pragma unroll
+                for (int ks = 0; ks < C::BKV / 32; ++ks) {
+                    if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
+                    acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
+                    av = avn;
+                    bv = bvn;
+                }
+                const int d = dbase + (lane & 15);
+                // the staged query tile goes to LDS first: its vmcnt wait then covers only loads
+                // (vmcnt retires in issue order), and these atomics have a whole tile of compute
+                // before the next wait
+                if (t0 == 0 && store_buf >= 0) lds_store_qtile(store_buf);
+                if (qd + C::BQ <= seqlen_q && head_dim == D) {
+                    // full tile (wave-uniform test): the four atomics without per-lane guards
+                    float *base = dqa + (int64_t)(qd + 16 * qh + 4 * g4) * dqa_row + d;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) atomicAdd(base + i * dqa_row, acc[i]);
+                } else if (d < head_dim) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int q = qd + 16 * qh + 4 * g4 + i;
+                        if (q < seqlen_q) atomicAdd(dqa + (int64_t)q * dqa_row + d, acc[i]);
+                    }
+                }
+            }
+        }
+    };
+
+    // step of tile `it` (LDS buffer BUF); itn, itnn: the next two live tiles (nqt if none);
+    // itp: the previous live tile (-1 if none), whose dQ this step computes
+    auto qstep = [&](auto par_tag, int itp, int it, int itn, int itnn) __attribute__((always_inline)) {
         constexpr int BUF = decltype(par_tag)::value;
         // half BUF loads tile itnn now; half 1-BUF writes tile itn (loaded a step ago) to LDS
         const bool my_load = stg_half == BUF, my_store = stg_half != BUF;
@@ -335,6 +390,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         const float *lse_b = lse_s + BUF * C::BQ;
         const float *del_b = del_s + BUF * C::BQ;
         const int q0 = q_begin + it * C::BQ;
+        char *dsw = dsimg + BUF * C::DS_IMG;
         if (my_load && itnn < nqt) gload_qtile(q_begin + itnn * C::BQ);
         // block sparsity: a dead 16-row half of a live tile is masked (P = 0 there)
         const bool dead0 = SPARSE && !row_live(q0 >> 4);
@@ -428,88 +484,63 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     u32x2 w = {T::pack2(ds[4 * g + 0], ds[4 * g + 1]), T::pack2(ds[4 * g + 2], ds[4 * g + 3])};
-                    lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), w);
+                    lds_write64(dsw, ds_off(32 * wave + l32, 8 * g + 4 * hi), w);
                 }
             }
         } else if (DQ) {
             // keys of this wave are all above the causal diagonal for this query tile: dS = 0
             const u32x2 z = {0u, 0u};
 #pragma unroll
-            for (int g = 0; g < 4; ++g) lds_write64(dsimg, ds_off(32 * wave + l32, 8 * g + 4 * hi), z);
+            for (int g = 0; g < 4; ++g) lds_write64(dsw, ds_off(32 * wave + l32, 8 * g + 4 * hi), z);
         }
+        const int store_buf = my_store && itn < nqt ? 1 - BUF : -1;
+        bool stored = false;
         if constexpr (DQ) {
-            __syncthreads();
-
-            // ---- dQ[q][d] += dS[q][key] K[key][d] over the BKV keys (16x16x32 MFMAs); the
-            // 2*(D/16) output tiles of 16 query rows x 16 columns are dealt round-robin to the waves,
-            // each summing over every key of the block, so one fp32 atomic per element per block.
-    #pragma unroll
-            for (int t0 = 0; t0 < 2 * (D / 16); t0 += C::NW) {
-                const int t = t0 + wave;
-                if (t < 2 * (D / 16)) {
-                    const int qh = t & 1;
-                    const int dbase = 16 * (t >> 1);
-                    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-                    auto dq_operands = [&](int ks, u32x4 &av, u32x4 &bv) __attribute__((always_inline)) {
-                        const int r0 = 32 * ks + 8 * g4 + qq;
-                        u32x2 a0 = lds_read_tr(dsimg, ds_off(r0, 16 * qh + 4 * pp));
-                        u32x2 a1 = lds_read_tr(dsimg, ds_off(r0 + 4, 16 * qh + 4 * pp));
-                        av = u32x4{a0[0], a0[1], a1[0], a1[1]};
-                        u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
-                        u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
-                        bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
-                    };
-                    // operands of key step ks+1 are read before the MFMA of step ks
-                    u32x4 av, bv, avn, bvn;
-                    dq_operands(0, av, bv);
-    #pragma unroll
-                    for (int ks = 0; ks < C::BKV / 32; ++ks) {
-                        if (ks + 1 < C::BKV / 32) dq_operands(ks + 1, avn, bvn);
-                        acc = T::mfma16(as_frag<T>(av), as_frag<T>(bv), acc);
-                        av = avn;
-                        bv = bvn;
-                    }
-                    const int d = dbase + (lane & 15);
-                    // the prefetched query tile goes to LDS first: its vmcnt wait then covers only
-                    // loads (vmcnt retires in issue order), and these atomics have a whole tile of
-                    // compute before the next wait
-                    if (t0 == 0 && my_store && itn < nqt) lds_store_qtile(1 - BUF);
-                    if (q0 + C::BQ <= seqlen_q && head_dim == D) {
-                        // full tile (wave-uniform test): the four atomics without per-lane guards
-                        float *base = dqa + (int64_t)(q0 + 16 * qh + 4 * g4) * dqa_row + d;
-    #pragma unroll
-                        for (int i = 0; i < 4; ++i) atomicAdd(base + i * dqa_row, acc[i]);
-                    } else if (d < head_dim) {
-    #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int q = q0 + 16 * qh + 4 * g4 + i;
-                            if (q < seqlen_q) atomicAdd(dqa + (int64_t)q * dqa_row + d, acc[i]);
-                        }
-                    }
-                }
+            // dQ runs one tile behind: the previous tile's dS image is complete since the barrier
+            // that closed the previous step, so each step needs a single barrier (the dS image of
+            // this tile is read in the next step, the other buffer)
+            if (itp >= 0) {
+                dq_phase(dsimg + (1 - BUF) * C::DS_IMG, q_begin + itp * C::BQ, store_buf);
+                stored = true;
             }
         }
-        // waves without a dQ tile (or kernels without dQ) store the prefetched tile here
-        if (my_store && itn < nqt && (!DQ || wave >= 2 * (D / 16))) lds_store_qtile(1 - BUF);
+        // waves without a dQ tile (or steps without a dQ phase) store the staged tile here
+        if (store_buf >= 0 && !(stored && wave < 2 * (D / 16))) lds_store_qtile(store_buf);
         __syncthreads();
     };
+    int ilast = -1, blast = 0;   // last tile and its buffer (its dQ runs after the walk)
     if constexpr (SPARSE) {
-        int it = t_first, itn = t_second;
+        int itp = -1, it = t_first, itn = t_second;
         while (it < nqt) {
             int itnn = itn < nqt ? next_qt(itn) : nqt;
-            qstep(I0(), it, itn, itnn);
+            qstep(I0(), itp, it, itn, itnn);
+            ilast = it; blast = 0;
+            itp = it;
             it = itn;
             itn = itnn;
             if (it >= nqt) break;
             itnn = itn < nqt ? next_qt(itn) : nqt;
-            qstep(I1(), it, itn, itnn);
+            qstep(I1(), itp, it, itn, itnn);
+            ilast = it; blast = 1;
+            itp = it;
             it = itn;
             itn = itnn;
         }
     } else {
         for (int it = 0; it < nqt; it += 2) {
-            qstep(I0(), it, it + 1, it + 2);
-            if (it + 1 < nqt) qstep(I1(), it + 1, it + 2, it + 3);
+            qstep(I0(), it - 1, it, it + 1, it + 2);
+            if (it + 1 < nqt) qstep(I1(), it, it + 1, it + 2, it + 3);
+        }
+        ilast = nqt - 1;
+        blast = (nqt - 1) & 1;
+    }
+    if constexpr (DQ) {
+        // dQ of the last tile (its dS image is complete since the last step's closing barrier)
+        if (ilast >= 0) {
+            if (blast)
+                dq_phase(dsimg + C::DS_IMG, q_begin + ilast * C::BQ, -1);
+            else
+                dq_phase(dsimg, q_begin + ilast * C::BQ, -1);
         }
     }
 
