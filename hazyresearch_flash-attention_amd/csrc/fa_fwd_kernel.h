@@ -40,18 +40,21 @@ namespace fa {
 #endif
 
 // NW = waves per workgroup (32 query rows each); chosen per launch (fa_kernels_impl.h).
-template <int D, int NW_>
+// KSPLIT: the two halves of the workgroup share its query rows and split the key range (intra-
+// workgroup split-K for short sequences, merged through LDS at the end).
+template <int D, int NW_, bool KSPLIT = false>
 struct FwdCfg {
     static constexpr int NW = NW_;                // waves per workgroup
     static constexpr int NT = 64 * NW;            // threads per workgroup
-    static constexpr int BM = 32 * NW;            // query rows per workgroup
+    static constexpr int NWR = KSPLIT ? NW / 2 : NW;   // waves per key group (distinct row blocks)
+    static constexpr int BM = 32 * NWR;           // query rows per workgroup
     static constexpr int BN = 64;                 // keys per iteration
     static constexpr int NC = D / 8;              // 16-B chunks per row
     static constexpr int TILE_BYTES = BN * D * 2;
     static constexpr int CPT = (BN * NC + NT - 1) / NT;   // staged chunks per thread per tile
     static constexpr int RNG_BYTES_PER_WAVE = 2 * 32 * 32 * 2;  // two 32x32 u16 images
     static constexpr int lds_bytes(bool dropout) {
-        return 4 * TILE_BYTES + (dropout ? NW * RNG_BYTES_PER_WAVE : 0);
+        return (KSPLIT ? 8 : 4) * TILE_BYTES + (dropout ? NW * RNG_BYTES_PER_WAVE : 0);
     }
 };
 
@@ -107,9 +110,10 @@ constexpr int fwd_waves_per_eu(int D, int NW, bool dropout, bool sparse) {
 
 #define FA_FWD_BOUNDS(NW) __launch_bounds__(64 * NW)
 
-template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
+template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false, bool KSPLIT = false>
 __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu(D, NW, DROPOUT, SPARSE)))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
-    using C = FwdCfg<D, NW>;
+    static_assert(!KSPLIT || (!CAUSAL && !DROPOUT && !SPARSE && NW % 2 == 0), "split-K: dense non-causal only");
+    using C = FwdCfg<D, NW, KSPLIT>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     constexpr float LN2 = 0.6931471805599453f;
@@ -149,7 +153,8 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31;
     const int hi = lane >> 5;
-    const int qw = q0 + 32 * wave;       // first query row of this wave
+    const int kgrp = KSPLIT ? wave / C::NWR : 0;   // key group (KSPLIT: half of the key range)
+    const int qw = q0 + 32 * (wave - kgrp * C::NWR);   // first query row of this wave
     const int qrow = qw + l32;           // the query row this lane owns
     const int head_dim = a.head_dim;
 
@@ -435,13 +440,17 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
     // Dense walk: K[j], V[j] in LDS buffer j & 1.
     // DMA: piece p (1 KiB = RPP rows of the tile image) is written by wave p % NW; lane l lands at
     // byte 16 l of the piece, i.e. row RPP p + l / NC, slot l % NC, which holds chunk slot ^ x(row)
+    // KSPLIT: each key group stages its own tiles (its own 4 tile buffers) with its NWR waves
     constexpr int PIECES = C::TILE_BYTES / 1024;
-    constexpr int PPW = (PIECES + NW - 1) / NW;
+    constexpr int DNW = C::NWR;
+    constexpr int PPW = (PIECES + DNW - 1) / DNW;
     constexpr int RPP = 1024 / (2 * D);
+    const int dwave = wave - kgrp * C::NWR;
+    char *const gsm = smem + kgrp * 4 * C::TILE_BYTES;
     int dma_k_off[PPW], dma_v_off[PPW];
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-        const int p = wave + NW * i;
+        const int p = dwave + DNW * i;
         const int r = RPP * p + lane / C::NC;
         const int c = (lane % C::NC) ^ S::x(r);
         const bool ok = c * 8 < head_dim;
@@ -456,8 +465,8 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
         __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < PPW; ++i) {
-            const int p = wave + NW * i;
-            if (PIECES % NW == 0 || p < PIECES) dma16(srd, off[i], j * step_bytes, lds_addr(buf + 1024 * p));
+            const int p = dwave + DNW * i;
+            if (PIECES % DNW == 0 || p < PIECES) dma16(srd, off[i], j * step_bytes, lds_addr(buf + 1024 * p));
         }
     };
     // stage the next K/V tiles: issue the DMA early, wait for it late
@@ -466,16 +475,21 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
         dma_tile(vsrd, dma_v_off, v_tile_step, vb_wr, jv);
     };
     auto stage_commit = [&]() __attribute__((always_inline)) { vmcnt0(); };
+    // KSPLIT: group g walks tiles [jbeg, jend) = the g-th half of the key range, both groups in
+    // the same number of steps (a group past its end only meets the barriers)
+    const int jhalf = KSPLIT ? (nt + 1) / 2 : nt;
+    const int jbeg = kgrp * jhalf;
+    const int jend = KSPLIT ? min(nt, jbeg + jhalf) : nt;
     auto step = [&](auto par_tag, int j) __attribute__((always_inline)) {
         constexpr int P = decltype(par_tag)::value;
-        char *kb_rd = smem + P * C::TILE_BYTES;
-        char *vb_rd = smem + (2 + P) * C::TILE_BYTES;
-        char *kb_wr = smem + (1 - P) * C::TILE_BYTES;
-        char *vb_wr = smem + (3 - P) * C::TILE_BYTES;
+        char *kb_rd = gsm + P * C::TILE_BYTES;
+        char *vb_rd = gsm + (2 + P) * C::TILE_BYTES;
+        char *kb_wr = gsm + (1 - P) * C::TILE_BYTES;
+        char *vb_wr = gsm + (3 - P) * C::TILE_BYTES;
         stage_issue(kb_wr, vb_wr, j + 1, j + 1);
         // causal: a wave whose 32 rows all lie above this key tile would add exactly nothing (every
         // P = 0, no rescale): it only stages its share of the next tile and meets the barrier
-        if (!CAUSAL || j * C::BN <= qw + 31) {
+        if ((!CAUSAL || j * C::BN <= qw + 31) && (!KSPLIT || j < jend)) {
             f32x16 s[2];
             qk(kb_rd, s);
             typename T::frag pf[2][2];
@@ -525,14 +539,53 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
             j = jn;
         }
     } else {
-        // prologue: K[0] -> kbuf0, V[0] -> vbuf0
-        stage_issue(smem, smem + 2 * C::TILE_BYTES, 0, 0);
+        // prologue: K[jbeg] -> kbuf0, V[jbeg] -> vbuf0 (of the key group)
+        stage_issue(gsm, gsm + 2 * C::TILE_BYTES, jbeg, jbeg);
         stage_commit();
         __syncthreads();
-        for (int j = 0; j < nt; j += 2) {
-            step(std::integral_constant<int, 0>(), j);
-            if (j + 1 < nt) step(std::integral_constant<int, 1>(), j + 1);
+        for (int u = 0; u < jhalf; u += 2) {
+            step(std::integral_constant<int, 0>(), jbeg + u);
+            if (u + 1 < jhalf) step(std::integral_constant<int, 1>(), jbeg + u + 1);
         }
+    }
+
+    if constexpr (KSPLIT) {
+        // merge the two key groups' partial states through LDS (the tile buffers are free after
+        // the last barrier): group 1 writes (O, l, m*c), group 0 rescales both to the larger max
+        // and goes on to the epilogue. A group that saw no key (m_thr = -inf) gets weight 0.
+        constexpr int NR = 16 * (D / 32);              // O registers per lane
+        float *xo = (float *)smem;                     // [row wave][NR / 4][lane][4]
+        float *xl = xo + C::NWR * NR * 64;             // [row wave][lane]
+        float *xm = xl + C::NWR * 64;
+        const float mcx = m_thr == -INFINITY ? -INFINITY : mc_row;
+        if (kgrp == 1) {
+#pragma unroll
+            for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 v = {o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]};
+                    *reinterpret_cast<f32x4 *>(xo + ((dwave * (NR / 4) + 4 * dt + g) * 64 + lane) * 4) = v;
+                }
+            xl[dwave * 64 + lane] = l_i;
+            xm[dwave * 64 + lane] = mcx;
+        }
+        __syncthreads();
+        if (kgrp == 1) return;
+        const float mc1 = xm[dwave * 64 + lane];
+        const float l1 = xl[dwave * 64 + lane];
+        const float mcm = fmaxf(mcx, mc1);
+        const float a0 = mcx == -INFINITY ? 0.f : fast_exp2(mcx - mcm);
+        const float a1 = mc1 == -INFINITY ? 0.f : fast_exp2(mc1 - mcm);
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(xo + ((dwave * (NR / 4) + 4 * dt + g) * 64 + lane) * 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[dt][4 * g + e] = o[dt][4 * g + e] * a0 + v[e] * a1;
+            }
+        l_i = l_i * a0 + l1 * a1;
+        if (mcm != -INFINITY) mc_row = mcm;
     }
 
     // ---- epilogue

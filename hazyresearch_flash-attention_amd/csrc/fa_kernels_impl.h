@@ -15,11 +15,11 @@
 namespace fa {
 
 
-template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false>
+template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false, bool KSPLIT = false>
 static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
-    using C = FwdCfg<D, NW>;
+    using C = FwdCfg<D, NW, KSPLIT>;
     const int lds = C::lds_bytes(DROPOUT);
-    auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT, NW, SPARSE>;
+    auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT, NW, SPARSE, KSPLIT>;
     FA_ENSURE_LDS(kern, lds);
     dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
     hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a, bm);
@@ -36,18 +36,30 @@ static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipSt
 // per CU) spread the same rows evenly. B4 H12 S2048 D64 (384 workgroups): 793 vs 728 TF/s; C5
 // (256 = one per CU) and C2 (192) keep 8 (808 vs 842, 424 vs 431). With dropout the kernel
 // needs ~168 registers: 8-wave workgroups then fit one per CU (two waves per SIMD), 4-wave
-// ones three per CU, and C3's forward runs 457 vs 369 TF/s. FA_FWD_NW=2|4|8 overrides the
-// choice for tuning.
-template <int D, bool DROPOUT>
+// ones three per CU, and C3's forward runs 457 vs 369 TF/s. FA_FWD_NW=1 (split-K)|2|4|8 overrides
+// the choice for tuning.
+//
+// Split-K (code 1, KSPLIT kernels): when the 8-wave grid has at most one workgroup per CU, each
+// workgroup's latency is the whole kernel, so the two halves of a workgroup take the same 128
+// query rows and half the keys each and merge at the end: twice the workgroups, half the tile
+// walk per wave. Taken when the doubled grid still lands evenly (at most one workgroup per CU,
+// or exactly two): C5 (256 -> 512 workgroups) 823 vs 803 TF/s; C2 (192 -> 384, half the CUs
+// would run two) measured 391 vs 432 and keeps the plain kernel. Dense non-causal D <= 64
+// without dropout only.
+#ifndef FA_FWD_KSPLIT
+#define FA_FWD_KSPLIT 1
+#endif
+template <int D, bool CAUSAL, bool DROPOUT>
 static int pick_fwd_waves(const FaFwdArgs &a) {
     static const int forced = [] {
         const char *e = getenv("FA_FWD_NW");
         return e ? atoi(e) : 0;
     }();
-    if (forced == 2 || forced == 4 || forced == 8) return forced;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
     if (DROPOUT && D <= 64) return 4;
     const int64_t nwg8 = (int64_t)((a.max_seqlen_q + 255) / 256) * a.nheads * a.batch;
     const int cus = device_cus();
+    if (FA_FWD_KSPLIT && !CAUSAL && D <= 64 && cus > 0 && (2 * nwg8 <= cus || 2 * nwg8 == 2 * cus)) return 1;
     if (cus > 0 && nwg8 > cus && nwg8 < 2 * cus && nwg8 % cus != 0) return 4;
     return FA_FWD_NW_DEFAULT;
 }
@@ -55,7 +67,10 @@ static int pick_fwd_waves(const FaFwdArgs &a) {
 template <int D, typename T, bool CAUSAL, bool DROPOUT>
 static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
     if (bm.mask) return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8, true>(a, bm, stream);
-    switch (pick_fwd_waves<D, DROPOUT>(a)) {
+    switch (pick_fwd_waves<D, CAUSAL, DROPOUT>(a)) {
+        case 1:
+            if constexpr (!CAUSAL && !DROPOUT && D <= 64) return launch_fwd_nw<D, T, false, false, 8, false, true>(a, bm, stream);
+            return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
         case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
         case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, bm, stream);
         default: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 2>(a, bm, stream);

@@ -35,6 +35,8 @@ CONFIGS = [
     ("c5_B4_H16_1024x4096_D64", 4, 16, 1024, 4096, 64, False, "bf16"),
     ("bs_localglobal_B8_H12_S2048_D64", 8, 12, 2048, 2048, 64, False, "bf16"),   # fa_fwd_block
     ("c2_B8_H12_S512_D64_fp16", 8, 12, 512, 512, 64, False, "fp16"),
+    ("tiny_B1_H12_S2048_D64", 1, 12, 2048, 2048, 64, False, "bf16"),   # 96 workgroups of 8 waves
+    ("tiny_B2_H8_S1024_D64", 2, 8, 1024, 1024, 64, False, "bf16"),     # 64 workgroups of 8 waves
     ("c3_B8_H12_S2048_D64_causal_p0.1", 8, 12, 2048, 2048, 64, True, "bf16", 0.1),
     ("c3nd_B8_H12_S2048_D64_causal", 8, 12, 2048, 2048, 64, True, "bf16", 0.0),
 ]
