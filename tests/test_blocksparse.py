@@ -160,7 +160,10 @@ def test_blocksparse_full_layout_matches_dense():
     bsi = _bsi()
     from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func
     g = torch.Generator().manual_seed(3)
-    B, S, H, D = 2, 768, 4, 64
+    # H=24: 144 eight-wave workgroups, so the dense forward takes its plain 8-wave kernel (the same
+    # loop body as the block-sparse one; smaller grids take the split-K kernel, whose merge rounds
+    # differently)
+    B, S, H, D = 2, 768, 24, 64
     qkv = torch.randn(B * S, 3, H, D, generator=g).to(torch.float16).to(DEV)
     cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=DEV)
     layout = torch.ones((S + 15) // 16, (S + 255) // 256, dtype=torch.bool, device=DEV)
