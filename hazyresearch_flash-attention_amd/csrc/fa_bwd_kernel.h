@@ -446,9 +446,10 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                         const int slot = (r & 3) | (((r >> 2) & 1) << 2);
                         const uint32_t word = rw[r >> 3][slot >> 1];
                         const uint32_t rnd = (slot & 1) ? (word >> 16) : (word & 0xFFFFu);
-                        const bool keep = rnd <= keep_thr;
-                        dpv = keep ? dpv * rp : 0.f;
-                        pdv = keep ? p * rp : 0.f;
+                        // one select: the kept scale 1/(1-p) or 0, then two multiplies
+                        const float rpk = rnd <= keep_thr ? rp : 0.f;
+                        dpv = dpv * rpk;
+                        pdv = p * rpk;
                     }
                     sacc[r] = pdv;
                     zacc[r] = p * (dpv - del4[e]);
