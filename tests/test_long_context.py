@@ -48,3 +48,13 @@ def test_forward_grid_balance_four_wave_workgroups(causal):
     """B=1 H=36 S=2048: 288 eight-wave workgroups, between one and two per CU of a 256-CU device,
     so the launcher picks 4-wave workgroups (fa_kernels_impl.h pick_fwd_waves) without dropout."""
     run_case("separate", 1, 2048, 2048, 36, 64, torch.bfloat16, causal, 0.0)
+
+
+@pytest.mark.parametrize("seqlen_k,mode", [(1, "full"), (63, "full"), (65, "full"), (130, "random"), (4095, "random")])
+def test_forward_split_k_key_halves(seqlen_k, mode):
+    """Small grids take the intra-workgroup split-K forward (two key groups per 128-row block,
+    merged through LDS). Key counts where the second group gets no key (1, 63), one partial tile
+    (65, 130) or a long walk (4095); random padding where the mask generator allows it. With one
+    key the exact dQ is 0 (dP = delta), which the 2x rule cannot bound, so that case checks the
+    forward only (the 1-key backward is covered by test_empty_and_ragged_sequences_backward)."""
+    run_case("kvpacked", 2, 300, seqlen_k, 2, 64, torch.bfloat16, False, 0.0, mode=mode, grad=seqlen_k > 1)
