@@ -19,9 +19,6 @@
 
 namespace fa {
 
-#ifndef FA_BWD_DQ_XCD
-#define FA_BWD_DQ_XCD 1   // 1: XCD-aware block order (non-causal)
-#endif
 
 template <int D, int NW>
 struct DqCfg {
@@ -49,7 +46,7 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a
     if (CAUSAL) {
         qb = nqb - 1 - L / nbh;
         bh_lin = L % nbh;
-    } else if (FA_BWD_DQ_XCD) {
+    } else {
         // XCD-aware (as the forward): blocks L and L+8 share an XCD; each XCD gets a contiguous
         // run of (head, q-block), so a head's K/V stream through one L2 (bijective for any count)
         const int nwg = nqb * nbh;
@@ -57,9 +54,6 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a
         const int Lp = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
         qb = Lp % nqb;
         bh_lin = Lp / nqb;
-    } else {
-        qb = blockIdx.x;
-        bh_lin = blockIdx.y + gridDim.y * blockIdx.z;
     }
     const int h = bh_lin % a.nheads;
     const int b = bh_lin / a.nheads;

@@ -128,14 +128,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
     gstore128((uint16_t *)a.dq + row * a.dq_row_stride + h * a.dq_head_stride + c * 8, w);
 }
 
-#ifndef FA_BWD_MINW
-#define FA_BWD_MINW 2   // __launch_bounds__ minimum waves per SIMD (2: two workgroups per CU when causal)
-#endif
-#if FA_BWD_MINW > 0
-#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWaves<C>::value), FA_BWD_MINW)
-#else
-#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWaves<C>::value))
-#endif
+// two waves per SIMD: one 8-wave workgroup per CU, up to 256 registers per wave
+#define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWaves<C>::value), 2)
 // DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
 __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaBlockMask bm) {
