@@ -269,7 +269,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             // one lane offset for both rows' constants (the image offsets fold into the
             // instruction), so no per-buffer address stays live across the loop
             lds_write32(smem + C::OFF_LSE + buf * C::BQ * 4, 4 * sl, lse_st * LOG2E);
-            lds_write32(smem + C::OFF_DELTA + buf * C::BQ * 4, 4 * sl, del_st);
+            lds_write32(smem + C::OFF_DELTA + buf * C::BQ * 4, 4 * sl, -del_st);   // -delta
         }
     };
     // ---- block sparsity (fa_bwd_block): this workgroup's keys lie in one 256-key column block
@@ -417,9 +417,23 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         };
         if (active) {
             // ---- S = Q K^T and dZ = dO V^T : lane = key, registers = query rows crow(r,hi)
+            // without dropout dZ's accumulator starts at -delta of its row (the image holds -delta) (16-B LDS reads straight
+            // into the accumulator registers), so dS = P (dZ - delta) is one multiply per element
             f32x16 sacc, zacc;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; zacc[r] = 0.f; }
+            for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+            constexpr bool SEED_DZ = !DROPOUT;
+            if constexpr (!SEED_DZ) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) zacc[r] = 0.f;
+            } else {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 del4 = *reinterpret_cast<const f32x4 *>(del_b + 8 * g + 4 * hi);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) zacc[4 * g + e] = del4[e];
+                }
+            }
 #pragma unroll
             for (int ks = 0; ks < D / 16; ++ks) {
                 u32x4 qa = lds_read128(qimg, S::off(l32, 2 * ks + hi));
@@ -471,7 +485,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                         pdv = p * rpk;
                     }
                     sacc[r] = pdv;
-                    zacc[r] = p * (dpv - del4[e]);
+                    zacc[r] = SEED_DZ ? p * dpv : p * (dpv + del4[e]);
                 }
             }
             // packed 16-bit Pd and dS: the B operands of dV^T / dK^T and the dS image words

@@ -425,6 +425,8 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
             const char *doimg = smem + C::OFF_DO + (role_p ? QB : QBD) * C::Q_IMG;
             f32x16 x;
             const char *aimg = role_p ? qimg : doimg;
+            // (dZ's accumulator seeded with -delta, as fa_bwd_kernel does without dropout, measured
+            // 3-6 % slower in this kernel: C4 backward 4.01 vs 3.77 ms)
 #pragma unroll
             for (int r = 0; r < 16; ++r) x[r] = 0.f;
 #pragma unroll
