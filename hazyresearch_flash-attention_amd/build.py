@@ -19,8 +19,18 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 BUILD = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "flash_attn", "libfa_hip.so")
 
-SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_padding.hip", "fa_rotary.hip", "fa_d32.hip", "fa_d64.hip", "fa_d128.hip"]
-SOURCE_FLAGS = {}   # per-source extra compiler flags
+KERNEL_TUS = ["fa_d32_fwd.hip", "fa_d64_fwd.hip", "fa_d128_fwd.hip", "fa_d32_bwd.hip", "fa_d64_bwd.hip", "fa_d128_bwd.hip"]
+SOURCES = ["fa_api.cpp", "fa_aux.hip", "fa_padding.hip", "fa_rotary.hip"] + KERNEL_TUS
+# Per-source machine-scheduler choice, from one-process A/Bs of every LLVM AMDGPU strategy
+# (DESIGN 7.4): the forward kernels with the AMDGPU register-pressure trackers (north star +2 %,
+# C2 +4 %), the D=32 and D=128 backward with the iterative ILP scheduler (-5 %, -2…3 %); the D=64
+# backward keeps the default (every alternative even or slower on C3).
+_TRACKERS = ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]
+_ITILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+SOURCE_FLAGS = {
+    "fa_d32_fwd.hip": _TRACKERS, "fa_d64_fwd.hip": _TRACKERS, "fa_d128_fwd.hip": _TRACKERS,
+    "fa_d32_bwd.hip": _ITILP, "fa_d128_bwd.hip": _ITILP,
+}
 ARCH = os.environ.get("FA_OFFLOAD_ARCH", "gfx950")
 
 

@@ -1,0 +1,3 @@
+// Backward kernels for head-dim tile 128.
+#include "fa_kernels_impl.h"
+FA_INSTANTIATE_BWD(128)

@@ -139,11 +139,16 @@ static hipError_t launch_bwd_dt(const FaBwdArgs &a, const FaBlockMask &bm, hipSt
 
 }  // namespace fa
 
-#define FA_INSTANTIATE(D)                                                                        \
+// One translation unit per head-dim tile and direction, so each compiles in parallel and can
+// take its own scheduler flags (build.py SOURCE_FLAGS)
+#define FA_INSTANTIATE_FWD(D)                                                                    \
     namespace fa {                                                                               \
     template <> hipError_t launch_fwd<D>(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t s) { \
         return a.dtype == FA_DTYPE_BF16 ? launch_fwd_dt<D, Bf16>(a, bm, s) : launch_fwd_dt<D, Fp16>(a, bm, s); \
     }                                                                                            \
+    }
+#define FA_INSTANTIATE_BWD(D)                                                                    \
+    namespace fa {                                                                               \
     template <> hipError_t launch_bwd<D>(const FaBwdArgs &a, const FaBlockMask &bm, hipStream_t s) { \
         return a.dtype == FA_DTYPE_BF16 ? launch_bwd_dt<D, Bf16>(a, bm, s) : launch_bwd_dt<D, Fp16>(a, bm, s); \
     }                                                                                            \

@@ -48,7 +48,7 @@ def build(names):
     fb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(fb)
     fb.build(verbose=False)
-    VAR_TUS = ("fa_d32.hip", "fa_d64.hip", "fa_d128.hip")
+    VAR_TUS = tuple(fb.KERNEL_TUS)
     shared = [os.path.join(BUILD, s + ".o") for s in fb.SOURCES if s not in VAR_TUS]
 
     def one(name):

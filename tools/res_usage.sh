@@ -1,6 +1,7 @@
 #!/bin/bash
 # Print register / spill usage of the forward kernels of one head-dim TU under extra -D flags.
-#   tools/res_usage.sh <d32|d64|d128> [kernel-substring] [-DFOO=1 ...]
+#   tools/res_usage.sh <d32|d64|d128>_<fwd|bwd> [kernel-substring] [-DFOO=1 ...]
+# (build.py SOURCE_FLAGS are not applied: pass them as extra flags)
 TU=$1; shift
 MFMAFORM=${MFMAFORM--mllvm -amdgpu-mfma-vgpr-form}
 PAT=${1:-fa_fwd_kernel}; shift
