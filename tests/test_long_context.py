@@ -8,10 +8,12 @@ the reference's 2x rule (tests/test_flash_attn.py:407-409) on outputs, attention
 and dQ/dK/dV (run_case in test_flash_attn.py), at batch/head counts the oracle finishes in a few
 seconds on the GPU.
 """
+import math
+
 import pytest
 import torch
 
-from test_flash_attn import run_case
+from test_flash_attn import _fa, DEV, run_case
 
 pytestmark = pytest.mark.gpu
 
@@ -58,3 +60,78 @@ def test_forward_split_k_key_halves(seqlen_k, mode):
     key the exact dQ is 0 (dP = delta), which the 2x rule cannot bound, so that case checks the
     forward only (the 1-key backward is covered by test_empty_and_ragged_sequences_backward)."""
     run_case("kvpacked", 2, 300, seqlen_k, 2, 64, torch.bfloat16, False, 0.0, mode=mode, grad=seqlen_k > 1)
+
+
+def _attn_rows(q, k, v, r0, upcast, reorder_ops):
+    """attention_ref (oracle/attention_ref.py:49-74; causal, no padding, no dropout) for the query
+    rows r0 .. r0 + C - 1 of a longer sequence: the top-left causal mask shifted by r0 (row i sees
+    keys <= r0 + i). Returns (output, fp32 scores) in the same layouts as attention_ref."""
+    dtype_og = q.dtype
+    if upcast:
+        q, k, v = q.float(), k.float(), v.float()
+    d = q.shape[-1]
+    if not reorder_ops:
+        scores = torch.einsum("bthd,bshd->bhts", q / math.sqrt(d), k)
+    else:
+        scores = torch.einsum("bthd,bshd->bhts", q, k / math.sqrt(d))
+    cm = torch.triu(torch.ones(q.shape[1], k.shape[1], dtype=torch.bool, device=q.device), r0 + 1)
+    scores.masked_fill_(cm, float("-inf"))
+    attention = torch.softmax(scores, dim=-1)
+    return torch.einsum("bhts,bshd->bthd", attention, v).to(dtype_og), scores
+
+
+@pytest.mark.parametrize("D", [64])
+def test_long_context_s65536_causal(D):
+    """S=65536 (the reference's "up to sequence length 64K", README.md:75), D=64 (atomic-dQ
+    backward) and D=128 (P/dS split backward + query-major dQ pass), causal, B=1 H=1,
+    forward (output, LSE) and backward (dQ, dK, dV) under the 2x rule. The full 64K x 64K score
+    matrix does not fit the oracle's one-shot form, so the oracle runs over 4096-row query chunks
+    (_attn_rows: the same expression with the causal mask shifted to the chunk's rows) and sums
+    dK/dV over the chunks."""
+    from flash_attn import flash_attn_hip as hip
+    fi = _fa()
+    S, H, C = 65536, 1, 4096
+    g = torch.Generator().manual_seed(7)
+    q, k, v, gout = (torch.randn(S, H, D, generator=g).bfloat16().to(DEV) for _ in range(4))
+    cu = torch.tensor([0, S], dtype=torch.int32, device=DEV)
+    qg, kg, vg = (t.clone().requires_grad_() for t in (q, k, v))
+    out = fi.flash_attn_unpadded_func(qg, kg, vg, cu, cu, S, S, 0.0, causal=True)
+    dq, dk, dv = torch.autograd.grad(out, (qg, kg, vg), gout)
+    _, lse = hip.fwd(q, k, v, cu, cu, S, S, 0.0, D ** -0.5, False, True, False, None)[:2]
+    torch.cuda.synchronize()
+
+    # fp32 leaves for the fp32 oracle, input-dtype leaves for the PyTorch baseline of the 2x rule
+    qf, kf, vf = (t.view(1, S, H, D).float().requires_grad_() for t in (q, k, v))
+    qb, kb, vb = (t.view(1, S, H, D).clone().requires_grad_() for t in (q, k, v))
+    gb = gout.view(1, S, H, D)
+    err = {n: 0.0 for n in ("out", "dq", "dk", "dv")}
+    base = dict(err)
+    dk_ref = torch.zeros(1, S, H, D, device=DEV)
+    dv_ref = torch.zeros_like(dk_ref)
+    dk_pt = torch.zeros_like(dk_ref)
+    dv_pt = torch.zeros_like(dk_ref)
+    for r0 in range(0, S, C):
+        o_ref, scores = _attn_rows(qf[:, r0:r0 + C], kf[:, :r0 + C], vf[:, :r0 + C], r0, upcast=True,
+                                   reorder_ops=False)
+        lse_ref = torch.logsumexp(scores, dim=-1)[0, 0]
+        assert torch.allclose(lse[0, 0, r0:r0 + C], lse_ref, atol=2e-3, rtol=1e-3), f"lse rows {r0}+"
+        del scores
+        o_pt, _ = _attn_rows(qb[:, r0:r0 + C], kb[:, :r0 + C], vb[:, :r0 + C], r0, upcast=False, reorder_ops=True)
+        o_k = out.view(1, S, H, D)[:, r0:r0 + C]
+        err["out"] = max(err["out"], (o_k.float() - o_ref.float()).abs().max().item())
+        base["out"] = max(base["out"], (o_pt.float() - o_ref.float()).abs().max().item())
+        gc = gb[:, r0:r0 + C]
+        rq, rk, rv = torch.autograd.grad(o_ref, (qf, kf, vf), gc.float())
+        pq, pk, pv = torch.autograd.grad(o_pt, (qb, kb, vb), gc)
+        dk_ref += rk.float(); dv_ref += rv.float(); dk_pt += pk.float(); dv_pt += pv.float()
+        sl = slice(r0, r0 + C)
+        err["dq"] = max(err["dq"], (dq.view(1, S, H, D)[:, sl].float() - rq[:, sl].float()).abs().max().item())
+        base["dq"] = max(base["dq"], (pq[:, sl].float() - rq[:, sl].float()).abs().max().item())
+        del o_ref, o_pt, rq, rk, rv, pq, pk, pv
+    # dK/dV: chunk sums in fp32 (the baseline's chunk grads are bf16, summed in fp32, rounded once)
+    err["dk"] = (dk.view(1, S, H, D).float() - dk_ref).abs().max().item()
+    err["dv"] = (dv.view(1, S, H, D).float() - dv_ref).abs().max().item()
+    base["dk"] = (dk_pt.bfloat16().float() - dk_ref).abs().max().item()
+    base["dv"] = (dv_pt.bfloat16().float() - dv_ref).abs().max().item()
+    for n in err:
+        assert err[n] <= 2 * base[n], f"{n}: max err {err[n]} > 2x baseline {base[n]}"
