@@ -80,7 +80,7 @@ def _attn_rows(q, k, v, r0, upcast, reorder_ops):
     return torch.einsum("bhts,bshd->bthd", attention, v).to(dtype_og), scores
 
 
-@pytest.mark.parametrize("D", [64])
+@pytest.mark.parametrize("D", [64, 128])
 def test_long_context_s65536_causal(D):
     """S=65536 (the reference's "up to sequence length 64K", README.md:75), D=64 (atomic-dQ
     backward) and D=128 (P/dS split backward + query-major dQ pass), causal, B=1 H=1,
