@@ -1,0 +1,1060 @@
+#!/usr/bin/env python3
+"""gen_fwd.py — generator of the hand-scheduled gfx950 FlashAttention forward kernel (head_dim <= 64).
+
+Writes one AMDGPU assembly file (code, kernel descriptor, metadata) for one dtype:
+
+    python gen_fwd.py --dtype bf16 --out fa_fwd_d64_bf16.s
+
+What the kernel computes is the forward of fa_fwd_kernel.h (and of the reference,
+csrc/flash_attn/src/fmha_fprop_kernel_1xN.h:453-681): for each (batch, head) and query row,
+O = softmax(scale * Q K^T) V over the keys of the row's sequence, and the natural-log LSE.
+Non-causal, no dropout: the shapes this kernel serves; the launcher keeps the HIP kernels for
+the others. Var-len sequences come through cu_seqlens exactly as in the HIP kernel.
+
+Why a generator: the D=64 forward is VALU-issue bound (per 32x64 score tile: 32 exp, 32 fma,
+16 cvt, 18 max3 against 16 MFMAs), so the instruction stream is placed by hand, the way
+cdna_hip_programming.md (Appendix B, "4-wave, one-wave-per-SIMD") describes:
+
+  * workgroup = 4 waves = 256 query rows, one wave per SIMD owning the whole register file;
+    each wave holds two 32-row query blocks A and B (every K/V fragment read feeds two MFMAs);
+  * S^T = K Q^T with v_mfma_f32_32x32x16 (lane = query row), O^T += V^T P^T with P straight
+    from registers, V^T fragments by ds_read_b64_tr_b16 (same fragment maps as fa_common.h);
+  * per 64-key tile two phases of 20 MFMAs: phase 1 = QK_B(j) + PV_B(j-1) beside block A's
+    softmax of tile j, phase 2 = QK_A(j+1) + PV_A(j) beside block B's softmax of tile j;
+  * row sums by a 16x16x32 MFMA of the 16-bit P against a 0/1 indicator matrix (4 per tile and
+    block, 16-cycle MFMAs) instead of 32 v_add_f32: the sum then covers the rounded P that the
+    P.V product uses;
+  * K/V tiles HBM -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds) into a 4-slot ring with a
+    3-tile prefetch distance, counted vmcnt, one s_barrier per tile;
+  * the deferred rescale (T13) of fa_fwd_kernel.h: the running max moves only when a tile max
+    passes it by 2^8 (one compare per tile; the rescale itself is an out-of-line block);
+  * fillers are distributed over the MFMA gaps by issue cost; a hazard pass inserts the
+    gfx950 wait states (measured from hipcc's own hazard recognizer: MFMA 32x32 -> read 12,
+    16x16 -> read 8, VALU -> MFMA 2, trans -> VALU 1, VALU -> permlane 2, m0 -> LDS-DMA 1)
+    and counted lgkmcnt waits.
+
+Nothing here writes through the scalar data cache: all stores are vector buffer stores.
+"""
+import argparse
+import math
+import os
+import sys
+
+# ------------------------------------------------------------------------------------------
+# geometry
+# ------------------------------------------------------------------------------------------
+D = 64                 # head-dim tile (head_dim <= 64 is zero-padded by the loads)
+BN = 64                # keys per tile
+R = 4                  # LDS ring slots (K and V each)
+DIST = 3               # DMA prefetch distance in tiles (tile t issues K(t+1+DIST), V(t+DIST))
+U = 4                  # loop unroll = lcm(R, 2 register buffers)
+TILE = BN * D * 2      # bytes per tile image
+KREG = 0
+VREG = R * TILE
+LDS_BYTES = 2 * R * TILE
+RESCALE_THR = 8.0      # log2-domain threshold of the deferred rescale (fa_fwd_kernel.h)
+OOB = 0x80000000
+
+# ---- VGPRs (arch)
+V_KADDR = 4            # 4: K fragment read address per k-step
+V_VADDR = 8            # 4: V^T fragment read address per (dt, half)
+V_DMA = 12             # 4: DMA source offsets: K piece 0, K piece 1, V piece 0, V piece 1
+V_S = {'A': 16, 'B': 48}        # 32 each: S^T accumulators (2 sub-tiles x 16)
+V_P = {'A': 80, 'B': 96}        # 16 each: P as 16-bit B operands
+V_MTHR = {'A': 112, 'B': 113}   # rescale threshold m + 2^8/c (raw score units)
+V_MC = {'A': 114, 'B': 115}     # m * c (log2 domain)
+V_TMP = {'A': 116, 'B': 124}    # 8 each
+V_BPA = 132            # ds_bpermute address: alpha of query (l&15)+16(l>>5)  (sum-MFMA lane map)
+V_BPL = 133            # ds_bpermute address: row sum of query l&31
+V_NEGINF = 134
+V_NVREL = 135          # last tile: valid keys of the tile minus 4*hi
+V_OOFF = {'A': 136, 'B': 140}   # 4 each: O store offsets (dt, g)
+V_LOFF = {'A': 144, 'B': 145}   # LSE store offset
+V_ONEF = 146           # 1.0f
+V_LANE = 147
+NVGPR = 148
+# ---- AGPRs
+A_O = {'A': 0, 'B': 32}         # O^T accumulators (2 d-blocks x 16)
+A_L = {'A': 64, 'B': 68}        # row-sum accumulators (16x16 MFMA C)
+A_ONES = 72                     # 0/1 indicator A operand of the row-sum MFMA
+A_Q = {'A': 76, 'B': 92}        # Q fragments (B operand of S^T = K Q^T), 4 k-steps x 4
+A_KF = 108                      # K fragments [buf 2][st*4+ks] x 4
+A_VF = 172                      # V^T fragments [buf 2][dt*4+st*2+s] x 4
+NAGPR = 236
+
+# ---- SGPRs
+S_KD, S_VD, S_QD, S_OD, S_LD = 8, 12, 16, 20, 24   # buffer descriptors (4 each)
+S_C, S_THR, S_J, S_NT, S_LAST = 28, 29, 30, 31, 32
+S_KSTEP, S_VSTEP, S_WAVE = 35, 36, 37
+S_M0B = 38             # 1024 * wave: this wave's DMA pieces start at piece `wave`
+S_ARG = 40             # kernel arguments s[40:75]
+S_CU = 76              # cu_seqlens values s[76:79]
+S_T = 80               # temporaries s[80:97]
+NSGPR = 98
+
+
+class Inst:
+    """One instruction (or an unbreakable group of lines).
+
+    kind: mfma | valu | trans | perm | accr | accw | ds | dma | vload | vstore | salu | m0 |
+          smem | wait | nop | br | label | barrier | raw
+    cost: issue cycles used by the gap placer. rd / wr: register names ('v12', 'a40', 's3',
+    'vcc', 'm0'). rdc: MFMA srcC registers. pipe: MFMA pipe cycles (32 or 16).
+    deadline: index of the MFMA (within its phase) that this filler must precede.
+    """
+    __slots__ = ('txt', 'kind', 'cost', 'rd', 'wr', 'rdc', 'pipe', 'deadline', 'lgkm_dst')
+
+    def __init__(self, txt, kind, cost=4, rd=(), wr=(), rdc=(), pipe=0, deadline=None):
+        self.txt, self.kind, self.cost = txt, kind, cost
+        self.rd, self.wr, self.rdc = frozenset(rd), frozenset(wr), frozenset(rdc)
+        self.pipe, self.deadline = pipe, deadline
+
+
+def rv(base, n=1):
+    return [f'v{base + i}' for i in range(n)]
+
+
+def ra(base, n=1):
+    return [f'a{base + i}' for i in range(n)]
+
+
+def vs(base, n=1):
+    return f'v{base}' if n == 1 else f'v[{base}:{base + n - 1}]'
+
+
+def as_(base, n=1):
+    return f'a{base}' if n == 1 else f'a[{base}:{base + n - 1}]'
+
+
+def V(txt, dst, srcs, kind='valu', cost=4):
+    """VALU with VGPR operands given as ints (register numbers) or names."""
+    def nm(x):
+        return f'v{x}' if isinstance(x, int) else x
+    wr = [nm(d) for d in (dst if isinstance(dst, (list, tuple)) else [dst])]
+    rd = [nm(s) for s in srcs]
+    return Inst(txt, kind, cost, rd=rd, wr=wr)
+
+
+def salu(txt, rd=(), wr=(), cost=2):
+    return Inst(txt, 'salu', cost, rd=rd, wr=wr)
+
+
+def label(name):
+    return Inst(f'{name}:', 'label', 0)
+
+
+def raw(txt, cost=0):
+    return Inst(txt, 'raw', cost)
+
+
+class Gen:
+    def __init__(self, dtype):
+        assert dtype in ('bf16', 'f16')
+        self.dtype = dtype
+        self.mf32 = 'v_mfma_f32_32x32x16_bf16' if dtype == 'bf16' else 'v_mfma_f32_32x32x16_f16'
+        self.mf16 = 'v_mfma_f32_16x16x32_bf16' if dtype == 'bf16' else 'v_mfma_f32_16x16x32_f16'
+        self.cvt = 'v_cvt_pk_bf16_f32' if dtype == 'bf16' else 'v_cvt_pk_f16_f32'
+        self.one2 = 0x3F803F80 if dtype == 'bf16' else 0x3C003C00
+        self.nlabel = 0
+        self.name = f'fa_fwd_d64_{dtype}_asm'
+
+    def lab(self, stem):
+        self.nlabel += 1
+        return f'.L{stem}_{self.nlabel}'
+
+    # ------------------------------------------------------------------ MFMA groups
+    def qk(self, X, t):
+        """S_X^T = K(t) Q_X^T: 2 sub-tiles x 4 k-steps (K fragment buffer t % 2)."""
+        out = []
+        S, Q = V_S[X], A_Q[X]
+        for st in range(2):
+            acc = S + 16 * st
+            for ks in range(4):
+                kf = A_KF + 32 * (t % 2) + 4 * (st * 4 + ks)
+                c = '0' if ks == 0 else vs(acc, 16)
+                out.append(Inst(f'{self.mf32} {vs(acc, 16)}, {as_(kf, 4)}, {as_(Q + 4 * ks, 4)}, {c}', 'mfma', 8,
+                                rd=ra(kf, 4) + ra(Q + 4 * ks, 4), wr=rv(acc, 16),
+                                rdc=rv(acc, 16) if ks else (), pipe=32))
+        return out
+
+    def pv_sum(self, X, t):
+        """O_X^T += V^T(t) P_X^T (8 MFMAs) interleaved with the 4 row-sum MFMAs.
+        Returns (list, {frag index: position in list})."""
+        out, use = [], {}
+        O, P, L = A_O[X], V_P[X], A_L[X]
+        sums = []
+        for st in range(2):
+            for s in range(2):
+                p = P + 4 * (st * 2 + s)
+                sums.append(Inst(f'{self.mf16} {as_(L, 4)}, {as_(A_ONES, 4)}, {vs(p, 4)}, {as_(L, 4)}', 'mfma', 8,
+                                 rd=ra(A_ONES, 4) + rv(p, 4), wr=ra(L, 4), rdc=ra(L, 4), pipe=16))
+        si = 0
+        for dt in range(2):
+            for st in range(2):
+                for s in range(2):
+                    f = dt * 4 + st * 2 + s
+                    vf = A_VF + 32 * (t % 2) + 4 * f
+                    p = P + 4 * (st * 2 + s)
+                    acc = O + 16 * dt
+                    use[f] = len(out)
+                    out.append(Inst(f'{self.mf32} {as_(acc, 16)}, {as_(vf, 4)}, {vs(p, 4)}, {as_(acc, 16)}', 'mfma', 8,
+                                    rd=ra(vf, 4) + rv(p, 4), wr=ra(acc, 16), rdc=ra(acc, 16), pipe=32))
+                if si < 4:
+                    out.append(sums[si])
+                    si += 1
+        return out, use
+
+    # ------------------------------------------------------------------ LDS reads / DMA
+    def kreads(self, t):
+        """K(t) fragments from ring slot t % R into buffer t % 2 (8 x ds_read_b128)."""
+        out = []
+        slot = KREG + (t % R) * TILE
+        for st in range(2):
+            for ks in range(4):
+                kf = A_KF + 32 * (t % 2) + 4 * (st * 4 + ks)
+                out.append(Inst(f'ds_read_b128 {as_(kf, 4)}, v{V_KADDR + ks} offset:{slot + st * 4096}', 'ds', 2,
+                                rd=[f'v{V_KADDR + ks}'], wr=ra(kf, 4)))
+        return out
+
+    def vreads(self, t):
+        """V(t)^T fragments from ring slot t % R into buffer t % 2 (16 x ds_read_b64_tr_b16).
+        Returns list of (frag, inst)."""
+        out = []
+        slot = VREG + (t % R) * TILE
+        for dt in range(2):
+            for st in range(2):
+                for s in range(2):
+                    f = dt * 4 + st * 2 + s
+                    vf = A_VF + 32 * (t % 2) + 4 * f
+                    for half in range(2):
+                        addr = V_VADDR + dt * 2 + half
+                        off = slot + (32 * st + 16 * s) * 128
+                        out.append((f, Inst(f'ds_read_b64_tr_b16 {as_(vf + 2 * half, 2)}, v{addr} offset:{off}', 'ds', 2,
+                                            rd=[f'v{addr}'], wr=ra(vf + 2 * half, 2))))
+        return out
+
+    def dma(self, kind, t):
+        """This wave's two 1-KiB pieces of the K or V tile t (LDS-DMA into ring slot t % R).
+        The descriptor walks the sequence: after each tile its base advances by 64 rows and
+        num_records shrinks by the same bytes, saturating at 0, so rows past the end (and every
+        tile past the last) read as zeros whatever the SGPR-offset range-check rule is."""
+        out = []
+        region = KREG if kind == 'K' else VREG
+        desc = S_KD if kind == 'K' else S_VD
+        step = S_KSTEP if kind == 'K' else S_VSTEP
+        dregs = [f's{desc + i}' for i in range(4)]
+        for i in range(2):
+            m0 = region + (t % R) * TILE + 4096 * i   # + 1024 * wave (S_M0B)
+            voff = V_DMA + (0 if kind == 'K' else 2) + i
+            out.append(Inst(f's_add_u32 m0, s{S_M0B}, {m0}', 'm0', 2, rd=[f's{S_M0B}'], wr=['m0', 'scc']))
+            out.append(Inst(f'buffer_load_dwordx4 v{voff}, s[{desc}:{desc + 3}], 0 offen lds', 'dma', 16,
+                            rd=[f'v{voff}', 'm0'] + dregs))
+        st = f's{step}'
+        out.append(salu(f's_add_u32 s{desc}, s{desc}, {st}', rd=[dregs[0], st], wr=[dregs[0], 'scc']))
+        out.append(salu(f's_addc_u32 s{desc + 1}, s{desc + 1}, 0', rd=[dregs[1], 'scc'], wr=[dregs[1], 'scc']))
+        out.append(salu(f's_sub_u32 s{desc + 2}, s{desc + 2}, {st}', rd=[dregs[2], st], wr=[dregs[2], 'scc']))
+        out.append(salu(f's_cselect_b32 s{desc + 2}, 0, s{desc + 2}', rd=[dregs[2], 'scc'], wr=[dregs[2]]))
+        return out
+
+    # ------------------------------------------------------------------ softmax of one tile
+    def softmax(self, X, masked, rescue):
+        """Block X's softmax of the tile in S_X: [mask], max tree, deferred-rescale test
+        (branch to an out-of-line block), exp2(s c - m c), conversion into P_X.
+        rescue: list that receives the out-of-line rescale block."""
+        S, P, T = V_S[X], V_P[X], V_TMP[X]
+        mthr, mc = V_MTHR[X], V_MC[X]
+        out = []
+        if masked:
+            for i in range(32):
+                st, r = divmod(i, 16)
+                kofs = 32 * st + (r & 3) + 8 * (r >> 2)
+                out.append(V(f'v_cmp_lt_i32 vcc, {kofs}, v{V_NVREL}', 'vcc', [V_NVREL]))
+                out.append(Inst(f'v_cndmask_b32 v{S + i}, v{V_NEGINF}, v{S + i}, vcc', 'valu', 4,
+                                rd=[f'v{V_NEGINF}', f'v{S + i}', 'vcc'], wr=[f'v{S + i}']))
+        # max tree: 4 chains of v_max3 (ILP 4), then merge, then the lane pair (l, l^32)
+        chains = []
+        for k in range(4):
+            c = [S + 8 * k + e for e in range(8)]
+            t = T + k
+            chains.append([V(f'v_max3_f32 v{t}, v{c[0]}, v{c[1]}, v{c[2]}', t, c[0:3]),
+                           V(f'v_max3_f32 v{t}, v{t}, v{c[3]}, v{c[4]}', t, [t, c[3], c[4]]),
+                           V(f'v_max3_f32 v{t}, v{t}, v{c[5]}, v{c[6]}', t, [t, c[5], c[6]]),
+                           V(f'v_max_f32 v{t}, v{t}, v{c[7]}', t, [t, c[7]])])
+        for step in range(4):
+            for k in range(4):
+                out.append(chains[k][step])
+        out.append(V(f'v_max3_f32 v{T + 4}, v{T}, v{T + 1}, v{T + 2}', T + 4, [T, T + 1, T + 2]))
+        out.append(V(f'v_max_f32 v{T + 4}, v{T + 4}, v{T + 3}', T + 4, [T + 4, T + 3]))
+        out.append(V(f'v_mov_b32 v{T + 5}, v{T + 4}', T + 5, [T + 4]))
+        out.append(Inst(f'v_permlane32_swap_b32 v{T + 4}, v{T + 5}', 'perm', 4,
+                        rd=[f'v{T + 4}', f'v{T + 5}'], wr=[f'v{T + 4}', f'v{T + 5}']))
+        out.append(V(f'v_max_f32 v{T + 6}, v{T + 4}, v{T + 5}', T + 6, [T + 4, T + 5]))
+        out.append(V(f'v_cmp_gt_f32 vcc, v{T + 6}, v{mthr}', 'vcc', [T + 6, mthr]))
+        resc, ret = self.lab(f'resc{X}'), self.lab(f'ret{X}')
+        # branch and its return label form one unbreakable group
+        # (it also carries the registers the out-of-line block touches, so the scheduler keeps
+        # their readers after it and anything unrelated may move across it)
+        touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], 32) + ra(A_L[X], 4)
+        out.append(Inst(f's_cbranch_vccnz {resc}\n{ret}:', 'br', 4, rd=['vcc'] + touched, wr=touched))
+        rescue.append(self.rescale_block(X, resc, ret))
+        # exp2(s * c - m * c), converted pairwise into the 16-bit P operand
+        for q in range(16):
+            a, b = S + 2 * q, S + 2 * q + 1
+            out.append(Inst(f'v_fma_f32 v{a}, v{a}, s{S_C}, -v{mc}', 'valu', 4, rd=[f'v{a}', f's{S_C}', f'v{mc}'],
+                            wr=[f'v{a}']))
+            out.append(Inst(f'v_fma_f32 v{b}, v{b}, s{S_C}, -v{mc}', 'valu', 4, rd=[f'v{b}', f's{S_C}', f'v{mc}'],
+                            wr=[f'v{b}']))
+            out.append(V(f'v_exp_f32 v{a}, v{a}', a, [a], kind='trans', cost=8))
+            out.append(V(f'v_exp_f32 v{b}, v{b}', b, [b], kind='trans', cost=8))
+            if q >= 1:
+                out.append(V(f'{self.cvt} v{P + q - 1}, v{S + 2 * q - 2}, v{S + 2 * q - 1}', P + q - 1,
+                             [S + 2 * q - 2, S + 2 * q - 1]))
+        out.append(V(f'{self.cvt} v{P + 15}, v{S + 30}, v{S + 31}', P + 15, [S + 30, S + 31]))
+        return out
+
+    def rescale_block(self, X, resc, ret):
+        """Out-of-line: lanes whose tile max passed the threshold move m (alpha = 2^(mc_old -
+        mc_new)), O_X and the row sums are scaled by alpha (the row-sum accumulator holds
+        query (l&15) + 16 (l>>5) in lane l: alpha is permuted to it)."""
+        T, mthr, mc = V_TMP[X], V_MTHR[X], V_MC[X]
+        O, L = A_O[X], A_L[X]
+        b = [label(resc), raw('s_nop 4')]
+        b.append(V(f'v_mul_f32 v{T + 7}, v{T + 6}, s{S_C}', T + 7, [T + 6]))
+        b.append(V(f'v_sub_f32 v{T}, v{mc}, v{T + 7}', T, [mc, T + 7]))
+        b.append(V(f'v_exp_f32 v{T}, v{T}', T, [T], kind='trans'))
+        b.append(V(f'v_add_f32 v{T + 1}, s{S_THR}, v{T + 6}', T + 1, [T + 6]))
+        b.append(Inst(f'v_cndmask_b32 v{T}, v{V_ONEF}, v{T}, vcc', 'valu', rd=[f'v{V_ONEF}', f'v{T}', 'vcc'],
+                      wr=[f'v{T}']))
+        b.append(Inst(f'v_cndmask_b32 v{mc}, v{mc}, v{T + 7}, vcc', 'valu', rd=[f'v{mc}', f'v{T + 7}', 'vcc'],
+                      wr=[f'v{mc}']))
+        b.append(Inst(f'v_cndmask_b32 v{mthr}, v{mthr}, v{T + 1}, vcc', 'valu', rd=[f'v{mthr}', f'v{T + 1}', 'vcc'],
+                      wr=[f'v{mthr}']))
+        for r in range(32):
+            t = T + 2 + (r % 4)
+            b.append(Inst(f'v_accvgpr_read_b32 v{t}, a{O + r}', 'accr', rd=[f'a{O + r}'], wr=[f'v{t}']))
+            b.append(V(f'v_mul_f32 v{t}, v{t}, v{T}', t, [t, T]))
+            b.append(Inst(f'v_accvgpr_write_b32 a{O + r}, v{t}', 'accw', rd=[f'v{t}'], wr=[f'a{O + r}']))
+        b.append(Inst(f'ds_bpermute_b32 v{T + 1}, v{V_BPA}, v{T}', 'ds', 2, rd=[f'v{V_BPA}', f'v{T}'], wr=[f'v{T + 1}']))
+        for r in range(4):
+            t = T + 2 + r
+            b.append(Inst(f'v_accvgpr_read_b32 v{t}, a{L + r}', 'accr', rd=[f'a{L + r}'], wr=[f'v{t}']))
+            b.append(V(f'v_mul_f32 v{t}, v{t}, v{T + 1}', t, [t, T + 1]))
+            b.append(Inst(f'v_accvgpr_write_b32 a{L + r}, v{t}', 'accw', rd=[f'v{t}'], wr=[f'a{L + r}']))
+        b.append(raw('s_nop 2'))
+        b.append(raw(f's_branch {ret}'))
+        return b
+
+    # ------------------------------------------------------------------ epilogue of a block
+    def epilogue(self, X):
+        """Normalise O_X by the row sum, store O (16-B stores after a permlane32 pair swap,
+        T21) and the LSE = (m c + log2 l) ln 2; an empty row (l == 0) gets 0 and -inf."""
+        S, T, mc = V_S[X], V_TMP[X], V_MC[X]
+        O, L = A_O[X], A_L[X]
+        e = []
+        e.append(Inst(f'v_accvgpr_read_b32 v{T}, a{L}', 'accr', rd=[f'a{L}'], wr=[f'v{T}']))
+        e.append(Inst(f'ds_bpermute_b32 v{T + 1}, v{V_BPL}, v{T}', 'ds', 2, rd=[f'v{V_BPL}', f'v{T}'], wr=[f'v{T + 1}']))
+        e.append(V(f'v_rcp_f32 v{T + 2}, v{T + 1}', T + 2, [T + 1], kind='trans', cost=8))
+        e.append(V(f'v_cmp_nlg_f32 vcc, 0, v{T + 1}', 'vcc', [T + 1]))
+        e.append(Inst(f'v_cndmask_b32 v{T + 2}, v{T + 2}, v{V_ONEF}, vcc', 'valu', rd=[f'v{T + 2}', f'v{V_ONEF}', 'vcc'],
+                      wr=[f'v{T + 2}']))
+        e.append(V(f'v_log_f32 v{T + 3}, v{T + 1}', T + 3, [T + 1], kind='trans', cost=8))
+        e.append(V(f'v_add_f32 v{T + 3}, v{T + 3}, v{mc}', T + 3, [T + 3, mc]))
+        e.append(V(f'v_mul_f32 v{T + 3}, 0x3f317218, v{T + 3}', T + 3, [T + 3]))
+        e.append(Inst(f'v_cndmask_b32 v{T + 3}, v{T + 3}, v{V_NEGINF}, vcc', 'valu', rd=[f'v{T + 3}', f'v{V_NEGINF}', 'vcc'],
+                      wr=[f'v{T + 3}']))
+        e.append(Inst(f'buffer_store_dword v{T + 3}, v{V_LOFF[X]}, s[{S_LD}:{S_LD + 3}], 0 offen', 'vstore', 8,
+                      rd=[f'v{T + 3}', f'v{V_LOFF[X]}']))
+        for dt in range(2):
+            for gi, g in enumerate((0, 2)):
+                # registers 4g..4g+7 of d-block dt hold d = 8g + 4hi + 0..3 and 8(g+1) + 4hi + 0..3
+                base = O + 16 * dt + 4 * g
+                E = S + (dt * 2 + gi) * 8          # 8 fp32 temps (S_X is dead by now)
+                Wb = V_P[X] + 4 * (dt * 2 + gi)    # 4 packed words (P_X is dead by now)
+                for k in range(8):
+                    e.append(Inst(f'v_accvgpr_read_b32 v{E + k}, a{base + k}', 'accr', rd=[f'a{base + k}'],
+                                  wr=[f'v{E + k}']))
+                for k in range(8):
+                    e.append(V(f'v_mul_f32 v{E + k}, v{E + k}, v{T + 2}', E + k, [E + k, T + 2]))
+                # a0 -> Wb+0 (regs 0,1), a1 -> Wb+1 (2,3), b0 -> Wb+2 (4,5), b1 -> Wb+3 (6,7)
+                for k in range(4):
+                    e.append(V(f'{self.cvt} v{Wb + k}, v{E + 2 * k}, v{E + 2 * k + 1}', Wb + k,
+                               [E + 2 * k, E + 2 * k + 1]))
+                # swap(a0, b0), swap(a1, b1): lanes 0-31 then hold d = 8g..8g+7 and lanes 32-63
+                # d = 8(g+1)..8(g+1)+7, in store order {a0', a1', b0', b1'} = Wb..Wb+3
+                e.append(Inst(f'v_permlane32_swap_b32 v{Wb + 0}, v{Wb + 2}', 'perm', 4, rd=[f'v{Wb}', f'v{Wb + 2}'],
+                              wr=[f'v{Wb}', f'v{Wb + 2}']))
+                e.append(Inst(f'v_permlane32_swap_b32 v{Wb + 1}, v{Wb + 3}', 'perm', 4, rd=[f'v{Wb + 1}', f'v{Wb + 3}'],
+                              wr=[f'v{Wb + 1}', f'v{Wb + 3}']))
+                e.append(Inst(f'buffer_store_dwordx4 {vs(Wb, 4)}, v{V_OOFF[X] + dt * 2 + gi}, s[{S_OD}:{S_OD + 3}], 0 offen',
+                              'vstore', 8, rd=rv(Wb, 4) + [f'v{V_OOFF[X] + dt * 2 + gi}']))
+        return e
+
+    # ------------------------------------------------------------------ phases
+    def phase1(self, t, masked=False, last=False, rescue=None):
+        """Tile t, phase 1: QK_B(t) + PV_B(t-1) + row sums beside block A's softmax of tile t,
+        K(t+1) fragment reads and the K(t+1+DIST) DMA."""
+        mf = self.qk('B', t) + self.pv_sum('B', t - 1)[0]
+        sm = self.softmax('A', masked, rescue)
+        side = [] if last else self.kreads(t + 1)
+        dma = [] if last else self.dma('K', t + 1 + DIST)
+        fill = merge(sm, [(i, x) for i, x in zip(spread(len(side), 27, len(sm) - 4), side)] +
+                     [(i, x) for i, x in zip(spread(len(dma), 6, len(sm) - 10), dma)])
+        return [mark()] + place(mf, fill)
+
+    def phase2(self, t, masked=False, last=False, rescue=None):
+        """Tile t, phase 2: QK_A(t+1) + PV_A(t) + row sums beside block B's softmax of tile t,
+        V(t) fragment reads (deadline: 3 MFMAs before their P.V MFMA) and the V(t+DIST) DMA."""
+        qk = [] if last else self.qk('A', t + 1)
+        pv, use = self.pv_sum('A', t)
+        mf = qk + pv
+        sm = self.softmax('B', masked, rescue)
+        vr = []
+        for f, ins in self.vreads(t):
+            ins.deadline = max(0, len(qk) + use[f] - 3)
+            vr.append(ins)
+        dma = [] if last else self.dma('V', t + DIST)
+        # the V reads go early (two per softmax instruction pair), the DMA pieces in the middle
+        fill = merge(sm, [(i, x) for i, x in zip(spread(len(vr), 1, 56), vr)] +
+                     [(i, x) for i, x in zip(spread(len(dma), 30, len(sm) - 10), dma)])
+        return [mark()] + place(mf, fill)
+
+
+def mark():
+    return Inst('', 'mark', 0)
+
+
+def spread(n, lo, hi):
+    """n positions spread evenly over [lo, hi)."""
+    if n == 0:
+        return []
+    hi = max(hi, lo + 1)
+    return [lo + (hi - lo) * k // n for k in range(n)]
+
+
+def merge(base, extra):
+    """Insert (position, inst) pairs into the list `base` (position = index in base before
+    which the extra instruction goes; stable for equal positions)."""
+    out = []
+    extra = sorted(extra, key=lambda p: p[0])
+    k = 0
+    for i, x in enumerate(base):
+        while k < len(extra) and extra[k][0] <= i:
+            out.append(extra[k][1])
+            k += 1
+        out.append(x)
+    out.extend(x for _, x in extra[k:])
+    return out
+
+
+def place(mfmas, fillers, window=10):
+    """Distribute the filler sequence over the gaps after each MFMA in proportion to the MFMA
+    pipe cycles; a filler with a deadline k is issued before MFMA k. Within that, a small list
+    scheduler may issue a later independent filler first when the next one would need wait
+    states (e.g. the permlane after the max tree)."""
+    M = len(mfmas)
+    if M == 0:
+        return schedule_run([], list(fillers), window)
+    total = sum(f.cost for f in fillers)
+    pipe = [m.pipe for m in mfmas]
+    P = float(sum(pipe))
+    out, acc, cum = [], 0.0, 0
+    rest = list(fillers)
+    for g in range(-1, M):
+        if g >= 0:
+            out.append(mfmas[g])
+            cum += pipe[g]
+        target = total * cum / P if g >= 0 else 0.0
+        if g == M - 1:
+            target = float('inf')
+        # every filler up to the last one whose deadline is g + 1 must be issued now
+        forced = -1
+        for i, f in enumerate(rest):
+            if f.deadline is not None and f.deadline <= g + 1:
+                forced = i
+        take = 0
+        a2 = acc
+        while take < len(rest) and (take <= forced or a2 + rest[take].cost * 0.5 <= target):
+            a2 += rest[take].cost
+            take += 1
+        chunk, rest = rest[:take], rest[take:]
+        acc = a2
+        out = schedule_run(out, chunk, window)
+    return out
+
+
+def conflicts(a, b):
+    """True if a and b may not be swapped (register dependences or control flow)."""
+    if a.kind in ('label', 'mark') or b.kind in ('label', 'mark'):
+        return True
+    ra_, wa = a.rd | a.rdc, a.wr
+    rb_, wb = b.rd | b.rdc, b.wr
+    return bool(wa & rb_ or wb & ra_ or wa & wb)
+
+
+def schedule_run(out, chunk, window):
+    """Append `chunk` (in order, but a filler may be issued ahead of at most `window` others it
+    does not depend on) to `out`, preferring fillers that need no wait states now."""
+    chunk = list(chunk)
+    while chunk:
+        pick = 0
+        if need_now(out, chunk[0]) > 0:
+            for j in range(1, min(window, len(chunk))):
+                c = chunk[j]
+                if any(conflicts(chunk[i], c) for i in range(j)):
+                    continue
+                if need_now(out, c) == 0:
+                    pick = j
+                    break
+        out.append(chunk.pop(pick))
+    return out
+
+
+def need_now(out, x, lookback=16):
+    """Wait states x would need if issued after `out` (writers within the last instructions)."""
+    need, dist = 0, 0
+    regs = set(x.rd) | set(x.rdc)
+    if x.kind == 'dma':
+        regs.add('m0')
+    for w in reversed(out[-lookback:]):
+        if w.kind in ('label', 'mark'):
+            continue
+        for reg in regs & w.wr:
+            need = max(need, need_states(w, x, reg) - dist)
+        dist += states_of(w)
+    return need
+
+
+# ------------------------------------------------------------------------------------------
+# hazard pass: wait states and counted waits along explicit control-flow paths
+# ------------------------------------------------------------------------------------------
+VALU_KINDS = ('valu', 'trans', 'perm', 'accr', 'accw', 'rfl')
+
+
+def states_of(x):
+    if x.kind in ('label', 'mark', 'wait'):
+        return 0
+    if x.kind in ('nop', 'raw') and x.txt.startswith('s_nop'):
+        return int(x.txt.split()[1]) + 1
+    if x.kind == 'raw' and (x.txt.startswith('s_waitcnt') or x.txt.endswith(':')):
+        return 0
+    return 1
+
+
+def need_states(w, r, reg):
+    """Minimum distance (in issued states; 1 = back to back) from writer w to reader r of reg:
+    the gfx950 wait states hipcc's hazard recognizer inserts, plus one."""
+    if w.kind == 'mfma':
+        if r.kind == 'mfma' and reg in r.rdc and w.wr == r.wr:
+            return 0                                   # same-accumulator chain
+        return 13 if w.pipe == 32 else 9               # s_nop 11 / s_nop 7
+    if w.kind in VALU_KINDS:
+        if reg.startswith('s') and r.kind in ('salu', 'm0', 'smem', 'dma', 'vload', 'vstore', 'br'):
+            return 6
+        if r.kind == 'mfma' or r.kind == 'perm':
+            return 3                                   # s_nop 1
+        if r.kind == 'rfl':
+            return 2                                   # s_nop 0 (v_readfirstlane / v_readlane)
+        if w.kind == 'trans' and r.kind in VALU_KINDS:
+            return 2                                   # s_nop 0
+        return 0
+    if w.kind == 'm0' and r.kind == 'dma':
+        return 2
+    return 0
+
+
+def parse_wait(txt):
+    """(vmcnt, lgkmcnt) limits of an s_waitcnt text (None = unconstrained)."""
+    vm = lg = None
+    for part in txt.replace(',', ' ').split()[1:]:
+        if part.startswith('vmcnt('):
+            vm = int(part[6:-1])
+        elif part.startswith('lgkmcnt('):
+            lg = int(part[8:-1])
+    return vm, lg
+
+
+def analyse(path):
+    """path: list of (block_list, index) references in execution order. Returns the list of
+    (block_list, index, Inst) insertions needed before the instruction at that index."""
+    ins = []
+    last_w = {}          # reg -> (state position, writer Inst)
+    pos = 0
+    lgkm = []            # outstanding DS / SMEM ops: (Inst, regs, phase_id)
+    vm = []              # outstanding vector-memory ops: (Inst, regs)
+    phase = 0
+    for blk, i in path:
+        x = blk[i]
+        if x.kind == 'mark':
+            phase += 1
+            continue
+        if x.kind in ('raw', 'wait') and x.txt.startswith('s_waitcnt'):
+            v_lim, l_lim = parse_wait(x.txt)
+            if l_lim is not None:
+                lgkm = lgkm[len(lgkm) - l_lim:] if l_lim < len(lgkm) else lgkm
+                if l_lim == 0:
+                    lgkm = []
+            if v_lim is not None:
+                vm = vm[len(vm) - v_lim:] if v_lim < len(vm) else vm
+                if v_lim == 0:
+                    vm = []
+            continue
+        if x.kind == 'raw' and x.txt.startswith('s_barrier'):
+            pos += 1
+            continue
+        regs = set(x.rd) | set(x.rdc)
+        touch = regs | set(x.wr)
+        # counted waits for outstanding LDS / vector-memory results
+        pre = []
+        k_l = max((k for k, (_, rr, _) in enumerate(lgkm) if rr & touch), default=-1)
+        if x.kind in ('ds', 'smem') and len(lgkm) >= 15:
+            k_l = max(k_l, 0)
+        if k_l >= 0:
+            younger = len(lgkm) - 1 - k_l
+            in_phase = sum(1 for (_, _, ph) in lgkm if ph == phase)
+            n = min(younger, in_phase)
+            if any(o.kind == 'smem' for (o, _, _) in lgkm[:k_l + 1]):
+                n = 0
+            pre.append(Inst(f's_waitcnt lgkmcnt({n})', 'wait', 0))
+            lgkm = lgkm[len(lgkm) - n:] if n else []
+        k_v = max((k for k, (_, rr) in enumerate(vm) if rr & touch), default=-1)
+        if k_v >= 0:
+            n = len(vm) - 1 - k_v
+            pre.append(Inst(f's_waitcnt vmcnt({n})', 'wait', 0))
+            vm = vm[len(vm) - n:] if n else []
+        # wait states
+        need = 0
+        for reg in regs:
+            if reg in last_w:
+                wp, w = last_w[reg]
+                need = max(need, need_states(w, x, reg) - (pos - wp))
+        if x.kind == 'dma' and 'm0' in last_w:
+            wp, w = last_w['m0']
+            need = max(need, need_states(w, x, 'm0') - (pos - wp))
+        if need > 0:
+            pre.append(Inst(f's_nop {need - 1}', 'nop', 4 * need))
+            pos += need
+        for p in pre:
+            ins.append((blk, i, p))
+        pos += states_of(x)
+        for reg in x.wr:
+            last_w[reg] = (pos - 1, x)
+        if x.kind in ('ds', 'smem'):
+            lgkm.append((x, set(x.wr), phase))
+        elif x.kind in ('dma', 'vload', 'vstore'):
+            vm.append((x, set(x.wr)))
+    return ins
+
+
+def apply_insertions(ins):
+    # one wait / nop of each sort per position: the strictest of the requests (a position can be
+    # reached along several paths or twice along one)
+    best = {}
+    for blk, i, p in ins:
+        key = (id(blk), i, p.txt.split()[0] + (p.txt.split('(')[0] if p.kind == 'wait' else ''))
+        if key not in best:
+            best[key] = (blk, i, p)
+        else:
+            q = best[key][2]
+            if p.kind == 'nop':
+                if int(p.txt.split()[1]) > int(q.txt.split()[1]):
+                    best[key] = (blk, i, p)
+            else:
+                if int(p.txt.split('(')[1][:-1]) < int(q.txt.split('(')[1][:-1]):
+                    best[key] = (blk, i, p)
+    ins = list(best.values())
+    by_blk = {}
+    for blk, i, p in ins:
+        by_blk.setdefault(id(blk), (blk, []))[1].append((i, p))
+    for blk, lst in by_blk.values():
+        grouped = {}
+        for i, p in lst:
+            grouped.setdefault(i, []).append(p)
+        for i in sorted(grouped, reverse=True):
+            blk[i:i] = grouped[i]
+    return len(ins)
+
+
+def fix_paths(paths, max_iter=400):
+    """Insert waits / nops until every path is clean (paths are rebuilt after each change,
+    since insertions move block indices)."""
+    total = 0
+    for _ in range(max_iter):
+        changed = 0
+        for mk in paths:
+            ins = analyse(mk())
+            if ins:
+                changed = apply_insertions(ins)
+                break
+        total += changed
+        if not changed:
+            return total
+    raise RuntimeError('hazard pass did not converge')
+
+
+def refs(blk):
+    return [(blk, i) for i in range(len(blk))]
+
+
+# ------------------------------------------------------------------------------------------
+# the kernel program
+# ------------------------------------------------------------------------------------------
+def S(txt, rd=(), wr=(), kind='salu'):
+    return Inst(txt, kind, 2, rd=rd, wr=wr)
+
+
+def xfun(dst, r, t1, t2):
+    """x(r) of the D=64 LDS swizzle (fa_common.h Swz<64>): u = (r>>1)&7, x = ((u&1)<<2)|(u>>1)."""
+    return [V(f'v_bfe_u32 v{t1}, v{r}, 1, 1', t1, [r]),
+            V(f'v_lshlrev_b32 v{t1}, 2, v{t1}', t1, [t1]),
+            V(f'v_bfe_u32 v{t2}, v{r}, 2, 2', t2, [r]),
+            V(f'v_or_b32 v{dst}, v{t1}, v{t2}', dst, [t1, t2])]
+
+
+def make_desc(d, ptr, start, rs, hs_lo, hs_hi, seqlen):
+    """Buffer descriptor s[d:d+3] for one (sequence, head): base = ptr + start*rs + h*hs (64-bit),
+    num_records = seqlen*rs bytes (rows past the sequence read as zero / drop their stores)."""
+    h = S_T + 9
+    return [S(f's_mul_i32 s92, s{start}, s{rs}'), S(f's_mul_hi_u32 s93, s{start}, s{rs}'),
+            S(f's_add_u32 s{d}, s{ptr}, s92'), S(f's_addc_u32 s{d + 1}, s{ptr + 1}, s93'),
+            S(f's_mul_i32 s92, s{h}, s{hs_lo}'), S(f's_mul_hi_u32 s93, s{h}, s{hs_lo}'),
+            S(f's_mul_i32 s94, s{h}, s{hs_hi}'), S('s_add_u32 s93, s93, s94'),
+            S(f's_add_u32 s{d}, s{d}, s92'), S(f's_addc_u32 s{d + 1}, s{d + 1}, s93'),
+            S(f's_mul_i32 s{d + 2}, s{seqlen}, s{rs}'), S(f's_mov_b32 s{d + 3}, 0x00020000')]
+
+
+WAVE_MODE = 'late'
+
+
+def wave_id_insts():
+    """Wave index within the workgroup (tid >> 6) into an SGPR. (gfx950: a v_readfirstlane
+    right behind the VALU that wrote its source reads the stale VGPR: the hazard pass keeps
+    them 2 states apart, as hipcc's s_nop 0 does.)"""
+    return [V('v_lshrrev_b32 v1, 6, v0', 1, [0]),
+            Inst(f'v_readfirstlane_b32 s{S_WAVE}, v1', 'rfl', rd=['v1'], wr=[f's{S_WAVE}'])]
+
+
+def prologue(g):
+    """Kernel arguments, (q-block, head, batch) of this workgroup (XCD-aware order as
+    fa_fwd_kernel.h), sequence bounds, buffer descriptors, per-lane addresses, Q loads, the first
+    DMAs, zeroed accumulators, and QK_A of tile 0."""
+    a = S_ARG   # s40 q, s42 k, s44 v, s46 o, s48 lse, s50 cu_q, s52 cu_k, s54 q_hs, s56 k_hs, s58 v_hs,
+    #             s60 o_hs, s62 q_rs, s63 k_rs, s64 v_rs, s65 o_rs, s66 nheads, s67 lse row bytes, s68 c,
+    #             s69 thr, s70 nqb, s71 nwg, s72 magic(nqb), s73 magic(nheads), s74 head_dim
+    p = []
+    p.append(Inst('s_load_dwordx16 s[40:55], s[0:1], 0x0', 'smem', 2, wr=[f's{i}' for i in range(40, 56)]))
+    p.append(Inst('s_load_dwordx16 s[56:71], s[0:1], 0x40', 'smem', 2, wr=[f's{i}' for i in range(56, 72)]))
+    p.append(Inst('s_load_dwordx4 s[72:75], s[0:1], 0x80', 'smem', 2, wr=[f's{i}' for i in range(72, 76)]))
+    p.append(raw('s_waitcnt lgkmcnt(0)'))
+    if WAVE_MODE == 'early':
+        p += wave_id_insts()
+    # L = x + nqb (y + H z); Lp = xcd q8 + min(xcd, r8) + (L >> 3); bh = Lp / nqb; b = bh / H
+    p += [S('s_mul_i32 s80, s66, s4'), S('s_add_u32 s80, s80, s3'), S('s_mul_i32 s80, s80, s70'),
+          S('s_add_u32 s80, s80, s2'),
+          S('s_and_b32 s81, s80, 7'), S('s_lshr_b32 s82, s71, 3'), S('s_and_b32 s83, s71, 7'),
+          S('s_mul_i32 s84, s81, s82'), S('s_min_u32 s85, s81, s83'), S('s_add_u32 s84, s84, s85'),
+          S('s_lshr_b32 s85, s80, 3'), S('s_add_u32 s84, s84, s85'),
+          S('s_lshl_b32 s85, s84, 1'), S('s_mul_hi_u32 s86, s85, s72'),
+          S('s_mul_i32 s87, s86, s70'), S('s_sub_u32 s87, s84, s87'),
+          S('s_lshl_b32 s85, s86, 1'), S('s_mul_hi_u32 s88, s85, s73'),
+          S('s_mul_i32 s89, s88, s66'), S('s_sub_u32 s89, s86, s89'),
+          S('s_lshl_b32 s90, s88, 2'),
+          S('s_add_u32 s92, s50, s90'), S('s_addc_u32 s93, s51, 0'),
+          Inst('s_load_dwordx2 s[76:77], s[92:93], 0x0', 'smem', 2, wr=['s76', 's77']),
+          S('s_add_u32 s94, s52, s90'), S('s_addc_u32 s95, s53, 0'),
+          Inst('s_load_dwordx2 s[78:79], s[94:95], 0x0', 'smem', 2, wr=['s78', 's79']),
+          raw('s_waitcnt lgkmcnt(0)')]
+    if WAVE_MODE != 'early':
+        p += wave_id_insts()
+    p += [S('s_sub_u32 s77, s77, s76'), S('s_sub_u32 s79, s79, s78'),
+          S('s_lshl_b32 s90, s87, 8'), S('s_cmp_ge_u32 s90, s77'), raw('s_cbranch_scc1 .Lend')]
+    # descriptors: K, V, Q, O, LSE
+    p += make_desc(S_KD, 42, 78, 63, 56, 57, 79)
+    p += make_desc(S_VD, 44, 78, 64, 58, 59, 79)
+    p += make_desc(S_QD, 40, 76, 62, 54, 55, 77)
+    p += make_desc(S_OD, 46, 76, 65, 60, 61, 77)
+    p += [S('s_mul_i32 s92, s88, s66'), S('s_add_u32 s92, s92, s89'),
+          S('s_mul_i32 s93, s92, s67'), S('s_mul_hi_u32 s94, s92, s67'),
+          S(f's_add_u32 s{S_LD}, s48, s93'), S(f's_addc_u32 s{S_LD + 1}, s49, s94'),
+          S(f's_lshl_b32 s{S_LD + 2}, s77, 2'), S(f's_mov_b32 s{S_LD + 3}, 0x00020000')]
+    p += [S(f's_mov_b32 s{S_C}, s68'), S(f's_mov_b32 s{S_THR}, s69'),
+          S(f's_add_u32 s{S_NT}, s79, 63'), S(f's_lshr_b32 s{S_NT}, s{S_NT}, 6'),
+          S(f's_sub_u32 s{S_LAST}, s{S_NT}, 1'), S(f's_mov_b32 s{S_J}, 0'),
+          S(f's_lshl_b32 s{S_KSTEP}, s63, 6'), S(f's_lshl_b32 s{S_VSTEP}, s64, 6'),
+          S(f's_lshl_b32 s{S_M0B}, s{S_WAVE}, 10')]
+    # ---- per-lane constants
+    L = V_LANE
+    p += [V(f'v_and_b32 v{L}, 63, v0', L, [0]), V('v_and_b32 v16, 31, v0', 16, [0]),
+          V('v_bfe_u32 v17, v0, 5, 1', 17, [0]), V('v_bfe_u32 v18, v0, 2, 2', 18, [0]),
+          V('v_and_b32 v19, 3, v0', 19, [0]), V('v_bfe_u32 v20, v0, 4, 1', 20, [0])]
+    p += xfun(21, 16, 22, 23)
+    for ks in range(4):   # K fragment reads: row l32, chunk 2ks + hi
+        p += [V(f'v_add_u32 v22, {2 * ks}, v17', 22, [17]), V('v_xor_b32 v22, v22, v21', 22, [22, 21]),
+              V('v_lshlrev_b32 v22, 4, v22', 22, [22]), V(f'v_lshl_add_u32 v{V_KADDR + ks}, v16, 7, v22', V_KADDR + ks, [16, 22])]
+    # V^T tr reads: row 4hi + qq + 8 half, column 32 dt + 16 grp + 4 pp
+    p += [V('v_lshl_add_u32 v24, v17, 2, v18', 24, [17, 18]), V('v_lshrrev_b32 v25, 1, v19', 25, [19]),
+          V('v_lshl_add_u32 v25, v20, 1, v25', 25, [20, 25]), V('v_and_b32 v26, 1, v19', 26, [19]),
+          V('v_lshlrev_b32 v26, 3, v26', 26, [26])]
+    for half in range(2):
+        p += [V(f'v_add_u32 v27, {8 * half}, v24', 27, [24])] + xfun(28, 27, 29, 30)
+        for dt in range(2):
+            p += [V(f'v_add_u32 v29, {4 * dt}, v25', 29, [25]), V('v_xor_b32 v29, v29, v28', 29, [29, 28]),
+                  V('v_lshl_or_b32 v29, v29, 4, v26', 29, [29, 26]),
+                  V(f'v_lshl_add_u32 v{V_VADDR + dt * 2 + half}, v27, 7, v29', V_VADDR + dt * 2 + half, [27, 29])]
+    p += [V(f'v_mov_b32 v{V_NEGINF}, 0xff800000', V_NEGINF, []), V(f'v_mov_b32 v{V_ONEF}, 1.0', V_ONEF, []),
+          V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
+    # DMA source offsets: pieces `wave` and `wave + 4` of a tile; lane l -> row 8p + l/8, slot l%8
+    p += [V(f'v_lshrrev_b32 v33, 3, v{L}', 33, [L]), V(f'v_and_b32 v34, 7, v{L}', 34, [L]),
+          S(f's_lshl_b32 s91, s{S_WAVE}, 3')]
+    for i in range(2):
+        p += [S(f's_add_u32 s92, s91, {32 * i}'), V('v_add_u32 v35, s92, v33', 35, [33])]
+        p += xfun(36, 35, 37, 38)
+        p += [V('v_xor_b32 v36, v34, v36', 36, [34, 36]), V('v_lshlrev_b32 v37, 3, v36', 37, [36]),
+              V('v_cmp_gt_u32 vcc, s74, v37', 'vcc', [37]),
+              V('v_mul_lo_u32 v38, v35, s63', 38, [35]), V('v_lshl_add_u32 v38, v36, 4, v38', 38, [36, 38]),
+              Inst(f'v_cndmask_b32 v{V_DMA + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'], wr=[f'v{V_DMA + i}']),
+              V('v_mul_lo_u32 v38, v35, s64', 38, [35]), V('v_lshl_add_u32 v38, v36, 4, v38', 38, [36, 38]),
+              Inst(f'v_cndmask_b32 v{V_DMA + 2 + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'],
+                   wr=[f'v{V_DMA + 2 + i}'])]
+    # Q load offsets (v43..v50), O store offsets, LSE offsets of blocks A (rows +0) and B (+32)
+    p += [S(f's_lshl_b32 s93, s{S_WAVE}, 6'), S('s_add_u32 s93, s93, s90')]
+    qoff = {'A': 43, 'B': 47}
+    for X, xo in (('A', 0), ('B', 32)):
+        p += [V('v_add_u32 v39, s93, v16', 39, [16])]
+        if xo:
+            p += [V(f'v_add_u32 v39, {xo}, v39', 39, [39])]
+        for ks in range(4):
+            p += [V(f'v_add_u32 v40, {2 * ks}, v17', 40, [17]), V('v_lshlrev_b32 v41, 3, v40', 41, [40]),
+                  V('v_cmp_gt_u32 vcc, s74, v41', 'vcc', [41]),
+                  V('v_mul_lo_u32 v42, v39, s62', 42, [39]), V('v_lshl_add_u32 v42, v40, 4, v42', 42, [40, 42]),
+                  Inst(f'v_cndmask_b32 v{qoff[X] + ks}, v31, v42, vcc', 'valu', rd=['v31', 'v42', 'vcc'],
+                       wr=[f'v{qoff[X] + ks}'])]
+        for dt in range(2):
+            for gi, gg in enumerate((0, 2)):
+                p += [V(f'v_add_u32 v40, {4 * dt + gg}, v17', 40, [17]), V('v_lshlrev_b32 v41, 3, v40', 41, [40]),
+                      V('v_cmp_gt_u32 vcc, s74, v41', 'vcc', [41]),
+                      V('v_mul_lo_u32 v42, v39, s65', 42, [39]), V('v_lshl_add_u32 v42, v40, 4, v42', 42, [40, 42]),
+                      Inst(f'v_cndmask_b32 v{V_OOFF[X] + dt * 2 + gi}, v31, v42, vcc', 'valu',
+                           rd=['v31', 'v42', 'vcc'], wr=[f'v{V_OOFF[X] + dt * 2 + gi}'])]
+        p += [V('v_cmp_eq_u32 vcc, 0, v17', 'vcc', [17]), V('v_lshlrev_b32 v42, 2, v39', 42, [39]),
+              Inst(f'v_cndmask_b32 v{V_LOFF[X]}, v31, v42, vcc', 'valu', rd=['v31', 'v42', 'vcc'],
+                   wr=[f'v{V_LOFF[X]}'])]
+    # ds_bpermute addresses and the 0/1 indicator of the row-sum MFMA
+    p += [V(f'v_and_b32 v40, 15, v{L}', 40, [L]), V(f'v_lshrrev_b32 v41, 5, v{L}', 41, [L]),
+          V('v_lshl_or_b32 v41, v41, 4, v40', 41, [41, 40]), V(f'v_lshlrev_b32 v{V_BPA}, 2, v41', V_BPA, [41]),
+          V(f'v_bfe_u32 v41, v{L}, 4, 1', 41, [L]), V('v_lshl_add_u32 v41, v41, 5, v40', 41, [41, 40]),
+          V(f'v_lshlrev_b32 v{V_BPL}, 2, v41', V_BPL, [41]),
+          V(f'v_bfe_u32 v41, v{L}, 4, 1', 41, [L]), V(f'v_bfe_u32 v42, v{L}, 3, 1', 42, [L]),
+          V('v_cmp_eq_u32 vcc, v41, v42', 'vcc', [41, 42]), V(f'v_mov_b32 v51, {g.one2:#x}', 51, []),
+          Inst('v_cndmask_b32 v51, v32, v51, vcc', 'valu', rd=['v32', 'v51', 'vcc'], wr=['v51'])]
+    p += [Inst(f'v_accvgpr_write_b32 a{A_ONES + r}, v51', 'accw', rd=['v51'], wr=[f'a{A_ONES + r}']) for r in range(4)]
+    # Q fragments
+    for X in 'AB':
+        for ks in range(4):
+            q = A_Q[X] + 4 * ks
+            p.append(Inst(f'buffer_load_dwordx4 {as_(q, 4)}, v{qoff[X] + ks}, s[{S_QD}:{S_QD + 3}], 0 offen', 'vload', 8,
+                          rd=[f'v{qoff[X] + ks}'], wr=ra(q, 4)))
+    # first DMAs: K0, [K1 V0], [K2 V1], [K3 V2] (tile t of the loop issues K(t+1+DIST), V(t+DIST))
+    p += g.dma('K', 0)
+    for t in range(DIST):
+        p += g.dma('K', t + 1) + g.dma('V', t)
+    # zero O, row sums, V fragment buffer 1 and P_B (PV_B(-1) of tile 0 adds nothing); m = -inf
+    p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(72)]
+    p += [Inst(f'v_accvgpr_write_b32 a{A_VF + 32 + r}, v32', 'accw', rd=['v32'], wr=[f'a{A_VF + 32 + r}'])
+          for r in range(32)]
+    p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
+    p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in (V_MTHR['A'], V_MTHR['B'], V_MC['A'], V_MC['B'])]
+    p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
+    # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
+    p += [raw('s_waitcnt vmcnt(8)'), raw('s_barrier')]
+    # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
+    p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
+    p += [raw('s_nop 7'), raw('s_nop 3')]
+    return p
+
+
+def dump_block(regs):
+    """Debug only (gen_fwd.py --dump): workgroup (0,0,0) stores the listed registers of every
+    wave into the O buffer as raw dwords [wave][reg][lane] (64-bit global stores), then ends."""
+    n = len(regs)
+    A0, A1, T = 140, 141, 142      # address pair and data temp (V_OOFF of block B: unused here)
+    b = [raw('s_waitcnt vmcnt(0) lgkmcnt(0)'), raw('s_nop 15'), raw('s_nop 15'),
+         S('s_or_b32 s96, s2, s3'), S('s_or_b32 s96, s96, s4'), S('s_cmp_eq_u32 s96, 0'),
+         raw('s_cbranch_scc1 .Ldump_go'), raw('s_endpgm'), label('.Ldump_go'),
+         S(f's_mul_i32 s96, s{S_WAVE}, {n * 256}'), raw('s_nop 3'),
+         V(f'v_lshlrev_b32 v{A0}, 2, v{V_LANE}', A0, [V_LANE]),
+         V(f'v_add_u32 v{A0}, s96, v{A0}', A0, [A0]),
+         V(f'v_mov_b32 v{A1}, s47', A1, []),
+         Inst(f'v_add_co_u32 v{A0}, vcc, s46, v{A0}', 'valu', rd=[f'v{A0}'], wr=[f'v{A0}', 'vcc']),
+         Inst(f'v_addc_co_u32 v{A1}, vcc, 0, v{A1}, vcc', 'valu', rd=[f'v{A1}', 'vcc'], wr=[f'v{A1}', 'vcc']),
+         raw('s_nop 3')]
+    for i, r in enumerate(regs):
+        src = r
+        if r.startswith('a'):
+            b.append(Inst(f'v_accvgpr_read_b32 v{T}, {r}', 'accr', rd=[r], wr=[f'v{T}']))
+            b.append(raw('s_nop 3'))
+            src = f'v{T}'
+        b.append(raw(f'global_store_dword v[{A0}:{A1}], {src}, off offset:{(i % 8) * 256}'))
+        b.append(raw('s_waitcnt vmcnt(0)'))
+        b.append(raw('s_nop 3'))
+        if i % 8 == 7:
+            b.append(Inst(f'v_add_co_u32 v{A0}, vcc, 0x800, v{A0}', 'valu', rd=[f'v{A0}'], wr=[f'v{A0}', 'vcc']))
+            b.append(Inst(f'v_addc_co_u32 v{A1}, vcc, 0, v{A1}, vcc', 'valu', rd=[f'v{A1}', 'vcc'], wr=[f'v{A1}', 'vcc']))
+            b.append(raw('s_nop 3'))
+    b += [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
+    return b
+
+
+DUMP = None   # (point, [registers]) set by --dump
+
+
+def last_tile(g, t, rescue):
+    """Tile t = nt - 1 (position t of the unrolled loop): masked softmax of both blocks, no
+    next-tile reads or DMA, then P.V of block B and the two epilogues."""
+    b = [label(f'.Llast{t}')]
+    tmp = V_TMP['A'] + 7
+    b += [S(f's_lshl_b32 s80, s{S_J}, 6'), S('s_sub_u32 s80, s79, s80'),
+          V(f'v_mov_b32 v{V_NVREL}, s80', V_NVREL, []),
+          V(f'v_bfe_u32 v{tmp}, v{V_LANE}, 5, 1', tmp, [V_LANE]),
+          V(f'v_lshlrev_b32 v{tmp}, 2, v{tmp}', tmp, [tmp]),
+          V(f'v_sub_u32 v{V_NVREL}, v{V_NVREL}, v{tmp}', V_NVREL, [V_NVREL, tmp])]
+    b += g.phase1(t, masked=True, last=True, rescue=rescue)
+    b += g.phase2(t, masked=True, last=True, rescue=rescue)
+    b += [mark()] + place(g.pv_sum('B', t)[0], g.epilogue('A'))
+    b += [mark()] + g.epilogue('B')
+    b += [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
+    return b
+
+
+def build(g):
+    rescue = []
+    pro = prologue(g)
+    if DUMP and DUMP[0] == 'pro':
+        pro += dump_block(DUMP[1])
+    tiles = []
+    for t in range(U):
+        blk = []
+        if t == 0:
+            blk.append(raw('.p2align 6'))
+            blk.append(label('.Lloop'))
+        blk += [S(f's_cmp_eq_u32 s{S_J}, s{S_LAST}'), raw(f's_cbranch_scc1 .Llast{t}')]
+        blk += g.phase1(t, rescue=rescue)
+        if DUMP and DUMP[0] == 'p1' and t == 0:
+            blk += dump_block(DUMP[1])
+        blk += g.phase2(t, rescue=rescue)
+        if DUMP and DUMP[0] == 'p2' and t == 0:
+            blk += dump_block(DUMP[1])
+        blk += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier'), S(f's_add_u32 s{S_J}, s{S_J}, 1')]
+        if t == U - 1:
+            blk.append(raw('s_branch .Lloop'))
+        tiles.append(blk)
+    lasts = [last_tile(g, t, rescue) for t in range(U)]
+    empty = [label('.Lempty'), mark()] + g.epilogue('A') + [mark()] + g.epilogue('B') + \
+            [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
+    end = [label('.Lend'), raw('s_endpgm')]
+    # control-flow paths for the hazard pass
+    paths = []
+    paths.append(lambda: refs(pro) + sum((refs(b) for b in tiles), []) + sum((refs(b) for b in tiles), []))
+    for t in range(U):
+        paths.append(lambda t=t: refs(pro) + sum((refs(b) for b in tiles), []) + sum((refs(b) for b in tiles[:t]), [])
+                     + refs(lasts[t]))
+    paths.append(lambda: refs(pro) + refs(empty))
+    # rescale blocks entered from their branch: the 40 instructions before it, the block, the rest
+    def resc_path(rb):
+        ret = rb[-1].txt.split()[-1]
+        for blk in tiles + lasts:
+            for i, x in enumerate(blk):
+                if x.kind == 'br' and x.txt.endswith(f'{ret}:'):
+                    lo = max(0, i - 40)
+                    return [(blk, k) for k in range(lo, i + 1)] + refs(rb) + [(blk, k) for k in range(i + 1, min(len(blk), i + 60))]
+        raise RuntimeError('rescale return not found')
+    for rb in rescue:
+        paths.append(lambda rb=rb: resc_path(rb))
+    n = fix_paths(paths)
+    blocks = [pro] + tiles + lasts + [empty, end] + rescue
+    return blocks, n
+
+
+def emit(g, blocks):
+    name = g.name
+    lines = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', '.amdhsa_code_object_version 5', '.text',
+             f'.globl {name}', '.p2align 8', f'.type {name},@function', f'{name}:']
+    for blk in blocks:
+        for x in blk:
+            if x.kind == 'mark' or not x.txt:
+                continue
+            if x.kind == 'label' or x.txt.startswith('.p2align'):
+                lines.append(x.txt)
+            else:
+                for ln in x.txt.split('\n'):
+                    lines.append(ln if ln.endswith(':') else '\t' + ln)
+    lines += ['.Lfunc_end:', f'\t.size {name}, .Lfunc_end-{name}', '',
+              '.rodata', '.p2align 6', f'.amdhsa_kernel {name}',
+              f'\t.amdhsa_group_segment_fixed_size {LDS_BYTES}',
+              '\t.amdhsa_private_segment_fixed_size 0',
+              f'\t.amdhsa_kernarg_size {KARG_BYTES}',
+              '\t.amdhsa_user_sgpr_count 2',
+              '\t.amdhsa_user_sgpr_kernarg_segment_ptr 1',
+              '\t.amdhsa_system_sgpr_workgroup_id_x 1',
+              '\t.amdhsa_system_sgpr_workgroup_id_y 1',
+              '\t.amdhsa_system_sgpr_workgroup_id_z 1',
+              '\t.amdhsa_system_vgpr_workitem_id 0',
+              f'\t.amdhsa_next_free_vgpr {NVGPR + NAGPR}',
+              f'\t.amdhsa_next_free_sgpr {NSGPR}',
+              f'\t.amdhsa_accum_offset {NVGPR}',
+              '\t.amdhsa_reserve_vcc 1',
+              '\t.amdhsa_float_denorm_mode_32 3',
+              '\t.amdhsa_float_denorm_mode_16_64 3',
+              '\t.amdhsa_dx10_clamp 1',
+              '\t.amdhsa_ieee_mode 0',
+              '.end_amdhsa_kernel', '',
+              '.amdgpu_metadata', '---', 'amdhsa.kernels:',
+              f'  - .agpr_count: {NAGPR}',
+              '    .args:', '      - .offset: 0', f'        .size: {KARG_BYTES}', '        .value_kind: by_value',
+              f'    .group_segment_fixed_size: {LDS_BYTES}',
+              '    .kernarg_segment_align: 8', f'    .kernarg_segment_size: {KARG_BYTES}',
+              '    .max_flat_workgroup_size: 256', f'    .name: {name}',
+              '    .private_segment_fixed_size: 0', f'    .sgpr_count: {NSGPR + 2}',
+              f'    .symbol: {name}.kd', f'    .vgpr_count: {NVGPR + NAGPR}', '    .wavefront_size: 64',
+              'amdhsa.target: amdgcn-amd-amdhsa--gfx950', 'amdhsa.version:', '  - 1', '  - 2', '...',
+              '.end_amdgpu_metadata', '']
+    return '\n'.join(lines)
+
+
+KARG_BYTES = 144
+
+
+def expand_regs(spec):
+    out = []
+    for part in spec.split(','):
+        if '-' in part:
+            f = part[0]
+            lo, hi = part[1:].split('-')
+            hi = hi.lstrip('vas')
+            out += [f'{f}{i}' for i in range(int(lo), int(hi) + 1)]
+        elif part:
+            out.append(part)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f16'])
+    ap.add_argument('--out', required=True)
+    ap.add_argument('--stats', action='store_true')
+    ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')
+    args = ap.parse_args()
+    global DUMP
+    if args.dump:
+        pt, regs = args.dump.split(':')
+        DUMP = (pt, expand_regs(regs))
+    g = Gen(args.dtype)
+    blocks, n = build(g)
+    txt = emit(g, blocks)
+    with open(args.out, 'w') as f:
+        f.write(txt)
+    if args.stats:
+        print(f'{args.out}: {sum(len(b) for b in blocks)} items, {n} waits/nops inserted')
+
+
+if __name__ == '__main__':
+    main()

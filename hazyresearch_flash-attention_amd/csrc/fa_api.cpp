@@ -90,7 +90,6 @@ int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {
             FaBwdArgs t{};
             t.head_dim = (int32_t)a;
             t.p_dropout = b ? 0.5f : 0.f;
-            t.max_seqlen_k = 1;
             const FaBlockMask m = {c ? (const uint8_t *)1 : nullptr, 0, 0, 0};
             return fa::bwd_dq_direct(t, m) ? 0 : 1;
         }
@@ -145,10 +144,14 @@ int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
     if ((int64_t)a->max_seqlen_q * a->q_row_stride * 2 >= lim || (int64_t)a->max_seqlen_k * a->k_row_stride * 2 >= lim ||
         (int64_t)a->max_seqlen_k * a->v_row_stride * 2 >= lim)
         return fail(FA_ERR_UNSUPPORTED, "fa_fwd: a sequence spans more than 2 GiB (seqlen * row_stride)");
+    if (a->impl != FA_IMPL_AUTO && a->impl != FA_IMPL_HIP)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: impl must be FA_IMPL_AUTO or FA_IMPL_HIP");
     if (a->max_seqlen_q == 0) return FA_OK;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
-    switch (pick_tile(a->head_dim)) {
+    if (fa::fwd_asm_eligible(*a, bm)) {
+        e = fa::launch_fwd_asm(*a, s);
+    } else switch (pick_tile(a->head_dim)) {
         case 32: e = fa::launch_fwd<32>(*a, bm, s); break;
         case 64: e = fa::launch_fwd<64>(*a, bm, s); break;
         default: e = fa::launch_fwd<128>(*a, bm, s); break;
@@ -169,7 +172,7 @@ int bwd_impl(const FaBwdArgs *a, const FaBlockMask &bm, void *stream) {
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: NULL tensor pointer");
     // the fp32 dQ workspace is only touched when dq is not written directly
     const bool direct = fa::bwd_dq_direct(*a, bm);
-    if (!direct && !a->dq_accum && a->max_seqlen_q > 0)
+    if (!direct && !a->dq_accum && a->max_seqlen_q > 0 && a->max_seqlen_k > 0)
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_bwd: dq_accum is NULL (required unless fa_query(FA_QUERY_BWD_WORKSPACE_NEEDED) is 0)");
     if (!aligned16(a->q) || !aligned16(a->k) || !aligned16(a->v) || !aligned16(a->dout) || !aligned16(a->out) ||
         !aligned16(a->dq) || !aligned16(a->dk) || !aligned16(a->dv) || (a->dq_accum && !aligned16(a->dq_accum)) ||
@@ -191,19 +194,31 @@ int bwd_impl(const FaBwdArgs *a, const FaBlockMask &bm, void *stream) {
         k_span * a->k_row_stride >= lim || k_span * a->v_row_stride >= lim ||
         k_span * a->dk_row_stride >= lim || k_span * a->dv_row_stride >= lim)
         return fail(FA_ERR_UNSUPPORTED, "fa_bwd: a sequence spans more than 2 GiB (seqlen * row_stride)");
-    // nothing to do without query rows: dq/dk/dv are the caller's (zero_tensors), softmax_d unused
-    if (a->max_seqlen_q == 0) return FA_OK;
     hipStream_t s = (hipStream_t)stream;
-    hipError_t e = fa::launch_bwd_pre(*a, s);
-    if (e != hipSuccess) return hip_fail(e, "fa_bwd pre launch");
-    if (a->max_seqlen_k > 0) {
-        switch (pick_tile(a->head_dim)) {
-            case 32: e = fa::launch_bwd<32>(*a, bm, s); break;
-            case 64: e = fa::launch_bwd<64>(*a, bm, s); break;
-            default: e = fa::launch_bwd<128>(*a, bm, s); break;
-        }
-        if (e != hipSuccess) return hip_fail(e, "fa_bwd launch");
+    hipError_t e;
+    // no query rows: no output depends on k or v, so dk = dv = 0 (softmax_d has no rows)
+    if (a->max_seqlen_q == 0) {
+        e = fa::launch_zero_seq_rows(a->dk, a->cu_seqlens_k, a->dk_row_stride, a->dk_head_stride, a->batch, a->nheads,
+                                     a->head_dim, a->max_seqlen_k, s);
+        if (e == hipSuccess)
+            e = fa::launch_zero_seq_rows(a->dv, a->cu_seqlens_k, a->dv_row_stride, a->dv_head_stride, a->batch,
+                                         a->nheads, a->head_dim, a->max_seqlen_k, s);
+        return e == hipSuccess ? FA_OK : hip_fail(e, "fa_bwd zero dk/dv launch");
     }
+    e = fa::launch_bwd_pre(*a, s);
+    if (e != hipSuccess) return hip_fail(e, "fa_bwd pre launch");
+    // no keys anywhere: the output is 0 and does not depend on q, so dq = 0 (softmax_d = 0 above)
+    if (a->max_seqlen_k == 0) {
+        e = fa::launch_zero_seq_rows(a->dq, a->cu_seqlens_q, a->dq_row_stride, a->dq_head_stride, a->batch, a->nheads,
+                                     a->head_dim, a->max_seqlen_q, s);
+        return e == hipSuccess ? FA_OK : hip_fail(e, "fa_bwd zero dq launch");
+    }
+    switch (pick_tile(a->head_dim)) {
+        case 32: e = fa::launch_bwd<32>(*a, bm, s); break;
+        case 64: e = fa::launch_bwd<64>(*a, bm, s); break;
+        default: e = fa::launch_bwd<128>(*a, bm, s); break;
+    }
+    if (e != hipSuccess) return hip_fail(e, "fa_bwd launch");
     if (!direct) {
         e = fa::launch_bwd_post(*a, s);
         if (e != hipSuccess) return hip_fail(e, "fa_bwd post launch");

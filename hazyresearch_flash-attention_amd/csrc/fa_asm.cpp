@@ -1,0 +1,150 @@
+// fa_asm.cpp — launcher of the hand-scheduled gfx950 assembly forward (csrc/asm/gen_fwd.py).
+//
+// The kernel is generated as AMDGPU assembly, assembled into a code object at build time
+// (build.py) and embedded in libfa_hip.so as a byte array (build/fa_asm_blobs.cpp). It is
+// loaded per device on first use with hipModuleLoadData and launched with hipModuleLaunchKernel
+// on the caller's stream (so it is captured into hipGraphs like the HIP kernels).
+//
+// It serves the north-star shape class: head_dim in (32, 64] (the D=64 tile), fp16/bf16,
+// non-causal, no dropout, dense (no block mask), no fused rotary. Everything else keeps the HIP
+// kernels of fa_fwd_kernel.h. Semantics are the same: var-len sequences through cu_seqlens,
+// rows past a sequence neither read nor written, LSE = m*scale + ln(sum) (-inf for no keys).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+
+#include "fa_launch.h"
+
+extern "C" {
+extern const unsigned char fa_asm_fwd_d64_bf16[];
+extern const unsigned long fa_asm_fwd_d64_bf16_size;
+extern const unsigned char fa_asm_fwd_d64_f16[];
+extern const unsigned long fa_asm_fwd_d64_f16_size;
+}
+
+namespace fa {
+
+// Kernel argument block; the byte offsets are the ones gen_fwd.py's prologue loads.
+struct FaAsmFwdArgs {
+    const void *q, *k, *v;
+    void *o;
+    float *lse;
+    const int32_t *cu_q, *cu_k;
+    uint64_t q_hs, k_hs, v_hs, o_hs;       // head strides, bytes
+    uint32_t q_rs, k_rs, v_rs, o_rs;       // row strides, bytes
+    uint32_t nheads;
+    uint32_t lse_row_bytes;                // lse_stride * 4
+    float c;                               // softmax_scale * log2(e)
+    float thr;                             // rescale threshold 2^8 in raw score units (8 / c)
+    uint32_t nqb;                          // 256-row query blocks per head (grid x)
+    uint32_t nwg;                          // workgroups in the grid
+    uint32_t magic_nqb;                    // ceil(2^32 / (2 nqb)): Lp / nqb = mulhi(2 Lp, magic)
+    uint32_t magic_h;                      // ceil(2^32 / (2 H))
+    uint32_t head_dim;
+    uint32_t pad;
+};
+static_assert(sizeof(FaAsmFwdArgs) == 144, "FaAsmFwdArgs layout (gen_fwd.py KARG_BYTES)");
+static_assert(offsetof(FaAsmFwdArgs, q_rs) == 88 && offsetof(FaAsmFwdArgs, c) == 112 &&
+              offsetof(FaAsmFwdArgs, magic_nqb) == 128 && offsetof(FaAsmFwdArgs, head_dim) == 136,
+              "FaAsmFwdArgs offsets (gen_fwd.py prologue)");
+
+namespace {
+
+constexpr int kRows = 256;            // query rows per workgroup
+constexpr int kMaxDev = 64;
+constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
+
+struct DevFns {
+    hipModule_t mod[2] = {nullptr, nullptr};
+    hipFunction_t fn[2] = {nullptr, nullptr};
+};
+std::mutex g_mu;
+DevFns g_fns[kMaxDev];
+
+hipError_t get_function(int dtype, hipFunction_t *out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    const int k = dtype == FA_DTYPE_BF16 ? 0 : 1;
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevFns &d = g_fns[dev];
+    if (!d.fn[k]) {
+        const void *img = k == 0 ? (const void *)fa_asm_fwd_d64_bf16 : (const void *)fa_asm_fwd_d64_f16;
+        const char *name = k == 0 ? "fa_fwd_d64_bf16_asm" : "fa_fwd_d64_f16_asm";
+        e = hipModuleLoadData(&d.mod[k], img);
+        if (e != hipSuccess) return e;
+        e = hipModuleGetFunction(&d.fn[k], d.mod[k], name);
+        if (e != hipSuccess) return e;
+    }
+    *out = d.fn[k];
+    return hipSuccess;
+}
+
+uint32_t magic_half(uint32_t d) {   // ceil(2^32 / (2 d)) for d >= 1
+    const uint64_t dd = 2ull * d;
+    return (uint32_t)(((1ull << 32) + dd - 1) / dd);
+}
+
+}  // namespace
+
+bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
+    if (a.impl == FA_IMPL_HIP) return false;
+    if (bm.mask || a.is_causal || a.p_dropout > 0.f || a.rot_cos) return false;
+    if (a.head_dim <= 32 || a.head_dim > 64) return false;
+    if (a.max_seqlen_q <= 0) return false;
+    // byte strides must fit the kernel's 32-bit row strides; the magic divisions are exact for
+    // n * d <= 2^30 (n < workgroups, d = q-blocks per head or heads)
+    const int64_t rs_max = (int64_t)1 << 31;
+    if (a.q_row_stride * 2 >= rs_max || a.k_row_stride * 2 >= rs_max || a.v_row_stride * 2 >= rs_max ||
+        a.o_row_stride * 2 >= rs_max || (int64_t)a.lse_stride * 4 >= rs_max)
+        return false;
+    const int64_t nqb = (a.max_seqlen_q + kRows - 1) / kRows;
+    const int64_t nwg = nqb * a.nheads * a.batch;
+    const int64_t dmax = nqb > a.nheads ? nqb : a.nheads;
+    if (nwg >= ((int64_t)1 << 30) / dmax) return false;
+    if (nqb > 65535 || a.nheads > 65535 || a.batch > 65535) return false;
+    return true;
+}
+
+hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
+    hipFunction_t fn = nullptr;
+    hipError_t e = get_function(a.dtype, &fn);
+    if (e != hipSuccess) return e;
+    FaAsmFwdArgs k;
+    std::memset(&k, 0, sizeof(k));
+    k.q = a.q;
+    k.k = a.k;
+    k.v = a.v;
+    k.o = a.o;
+    k.lse = a.softmax_lse;
+    k.cu_q = a.cu_seqlens_q;
+    k.cu_k = a.cu_seqlens_k;
+    k.q_hs = (uint64_t)a.q_head_stride * 2;
+    k.k_hs = (uint64_t)a.k_head_stride * 2;
+    k.v_hs = (uint64_t)a.v_head_stride * 2;
+    k.o_hs = (uint64_t)a.o_head_stride * 2;
+    k.q_rs = (uint32_t)(a.q_row_stride * 2);
+    k.k_rs = (uint32_t)(a.k_row_stride * 2);
+    k.v_rs = (uint32_t)(a.v_row_stride * 2);
+    k.o_rs = (uint32_t)(a.o_row_stride * 2);
+    k.nheads = (uint32_t)a.nheads;
+    k.lse_row_bytes = (uint32_t)a.lse_stride * 4;
+    k.c = a.softmax_scale * 1.4426950408889634f;
+    k.thr = kRescaleThr / k.c;
+    const uint32_t nqb = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
+    k.nqb = nqb;
+    k.nwg = nqb * (uint32_t)a.nheads * (uint32_t)a.batch;
+    k.magic_nqb = magic_half(nqb);
+    k.magic_h = magic_half((uint32_t)a.nheads);
+    k.head_dim = (uint32_t)a.head_dim;
+    size_t size = sizeof(k);
+    void *config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+    e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, kRows, 1, 1, 0, stream, nullptr, config);
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+}  // namespace fa

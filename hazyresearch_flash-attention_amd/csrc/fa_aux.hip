@@ -42,4 +42,30 @@ hipError_t launch_bwd_post(const FaBwdArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Zero the rows of every sequence of a (total, H, D) 16-bit tensor (any row / head stride):
+// one thread per 16-byte chunk. Used for gradients that have no contribution at all: dk/dv when
+// there are no query rows, dq when there are no keys.
+__global__ __launch_bounds__(256) void zero_seq_rows_kernel(uint16_t *base, const int32_t *cu, int64_t row_stride,
+                                                            int64_t head_stride, int head_dim) {
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int start = cu[b];
+    const int len = cu[b + 1] - start;
+    const int nc = head_dim / 8;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    const int row = idx / nc, c = idx % nc;
+    if (row >= len) return;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    gstore128(base + (int64_t)(start + row) * row_stride + (int64_t)h * head_stride + c * 8, z);
+}
+
+hipError_t launch_zero_seq_rows(void *base, const int32_t *cu, int64_t row_stride, int64_t head_stride, int batch,
+                                int nheads, int head_dim, int max_seqlen, hipStream_t s) {
+    if (max_seqlen <= 0 || batch <= 0 || nheads <= 0) return hipSuccess;
+    const int64_t chunks = (int64_t)max_seqlen * (head_dim / 8);
+    dim3 grid((unsigned)((chunks + 255) / 256), nheads, batch);
+    hipLaunchKernelGGL(zero_seq_rows_kernel, grid, dim3(256), 0, s, (uint16_t *)base, cu, row_stride, head_stride,
+                       head_dim);
+    return hipGetLastError();
+}
+
 }  // namespace fa

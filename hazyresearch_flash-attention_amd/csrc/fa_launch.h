@@ -31,9 +31,14 @@ hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t stream);
 constexpr bool bwd_dqk_tile(int D) { return FA_BWD_DQK && D >= FA_BWD_DQK_MIN_D; }
 inline bool bwd_dq_direct(const FaBwdArgs &a, const FaBlockMask &bm) {
     const int tile = a.head_dim <= 32 ? 32 : a.head_dim <= 64 ? 64 : 128;
-    return bwd_dqk_tile(tile) && a.p_dropout == 0.f && bm.mask == nullptr && a.max_seqlen_k > 0;
+    return bwd_dqk_tile(tile) && a.p_dropout == 0.f && bm.mask == nullptr;
 }
 hipError_t launch_bwd_post(const FaBwdArgs &a, hipStream_t stream);
+hipError_t launch_zero_seq_rows(void *base, const int32_t *cu, int64_t row_stride, int64_t head_stride, int batch,
+                                int nheads, int head_dim, int max_seqlen, hipStream_t s);
+// hand-scheduled assembly forward (fa_asm.cpp, csrc/asm/gen_fwd.py)
+bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm);
+hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream);
 
 // Raise a kernel's dynamic-LDS limit once per (kernel, device): the attribute is per device, so
 // a process that launches on several GPUs sets it on each. `done` is the call site's own bit set

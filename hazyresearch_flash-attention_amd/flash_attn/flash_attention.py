@@ -76,7 +76,7 @@ class FlashAttnRotaryQKVFunc(torch.autograd.Function):
             softmax_scale = D ** (-0.5)
         rng_state = _reserve(dropout_p, qkv.device)
         flat = qkv.view(B * S, 3, H, D)
-        cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=qkv.device)
+        cu = _uniform_cu_seqlens(B, S, qkv.device)
         out, lse = hip.fwd(flat[:, 0], k_rot.view(B * S, H, D), flat[:, 2], cu, cu, S, S, dropout_p, softmax_scale,
                            False, causal, False, None, rng_state=rng_state, rotary=(cos, sin))
         ctx.save_for_backward(qkv, k_rot, out, lse, cos, sin, cu)
@@ -99,6 +99,22 @@ class FlashAttnRotaryQKVFunc(torch.autograd.Function):
         st3 = (S * 3 * H * D, 3 * H * D, H * D, D)
         hip.rotary(dqkv, dqkv, cos, sin, (B, S, 3, H, D), st3, st3, 2, True)   # dq, dk back; dv as is
         return dqkv, None, None, None, None, None
+
+
+_cu_cache = {}
+
+
+def _uniform_cu_seqlens(B, S, device):
+    """cu_seqlens of B sequences of length S (cached per shape and device: one arange launch per
+    shape instead of one per call; the tensor is only read by the kernels)."""
+    key = (B, S, device)
+    cu = _cu_cache.get(key)
+    if cu is None:
+        cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=device)
+        if len(_cu_cache) > 64:
+            _cu_cache.clear()
+        _cu_cache[key] = cu
+    return cu
 
 
 class FlashMHA(nn.Module):
@@ -129,10 +145,15 @@ class FlashMHA(nn.Module):
         """x: (batch, seqlen, embed_dim); key_padding_mask: (batch, seqlen) bool."""
         qkv = self.Wqkv(x)
         b, s = qkv.shape[0], qkv.shape[1]
-        if (self.use_rotary_emb and qkv.is_cuda and qkv.is_contiguous() and key_padding_mask is None
-                and qkv.dtype in (torch.float16, torch.bfloat16)):
-            # fused rotary: q rotated inside the attention kernel, k by one half-size pass
+        fused = (self.use_rotary_emb and qkv.is_cuda and qkv.is_contiguous() and key_padding_mask is None
+                 and qkv.dtype in (torch.float16, torch.bfloat16) and self.head_dim % 8 == 0)
+        if fused:
             cos, sin = self.rotary_emb.cos_sin_tables(s, qkv.device, qkv.dtype)
+            # the kernel's Q load rotates all head_dim features: tables narrower than the head go
+            # through the separate pass below
+            fused = cos.shape[-1] >= self.head_dim and cos.shape[0] >= s
+        if fused:
+            # fused rotary: q rotated inside the attention kernel, k by one half-size pass
             dropout_p = self.inner_attn.dropout_p if self.inner_attn.training else 0.0
             context = FlashAttnRotaryQKVFunc.apply(qkv.view(b, s, 3, self.num_heads, self.head_dim), cos, sin,
                                                    dropout_p, self.inner_attn.softmax_scale, self.causal)

@@ -56,7 +56,12 @@ class FaFwdArgs(ctypes.Structure):
         ("rng_seed", _u64), ("rng_offset", _u64), ("rng_offset_dev", _vp),
         ("is_causal", _i32), ("dtype", _i32),
         ("rot_cos", _vp), ("rot_sin", _vp), ("rot_stride", _i64),
+        ("impl", _i32), ("reserved", _i32),
     ]
+
+
+FA_IMPL_AUTO = 0
+FA_IMPL_HIP = 1
 
 
 class FaBwdArgs(ctypes.Structure):
@@ -280,6 +285,11 @@ def reserve_rng(device, gen=None, increment=None):
             seed = gen.initial_seed()
             offset = gen.get_offset()
             gen.set_offset(offset + increment)
+        if offset + increment > GRAPH_RNG_BASE:
+            # eager offsets must stay below the captured sub-stream (and offset >> 2 within the
+            # kernels' 32-bit counter word), or eager and replayed dropout masks could repeat
+            raise RuntimeError("flash_attn: the CUDA generator's Philox offset passed 2^33; "
+                               "re-seed the generator (torch.cuda.manual_seed) to continue with dropout")
     return int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset), offset_dev
 
 
@@ -333,11 +343,12 @@ def _mask_struct(layout, dev):
 
 
 def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropout, softmax_scale,
-        zero_tensors, is_causal, return_softmax, gen, rng_state=None, layout=None, rotary=None):
+        zero_tensors, is_causal, return_softmax, gen, rng_state=None, layout=None, rotary=None, impl=FA_IMPL_AUTO):
     """Forward pass; same arguments and result as the reference's `flash_attn_cuda.fwd`.
     `layout` (optional, 0/1 (seqlen/16, seqlen/256) on the device) selects the block-sparse kernel.
     `rotary` (optional (cos, sin) tables, (>= max_seqlen_q, >= D) in q's dtype) rotates q inside
-    the kernel at its load (fused rotary, rotary.py:31-41); k must come rotated already."""
+    the kernel at its load (fused rotary, rotary.py:31-41); k must come rotated already.
+    `impl` (FA_IMPL_AUTO / FA_IMPL_HIP) picks the kernel family (include/fa_hip.h)."""
     qdt = q.dtype
     dt = _dtype_code(qdt)
     _check(k.dtype == qdt and v.dtype == qdt, "q, k, v must have the same dtype")
@@ -407,7 +418,7 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
             batch, nheads, head_dim, max_seqlen_q, max_seqlen_k, lse_stride,
             s.shape[2] if s is not None else 0, s.shape[3] if s is not None else 0,
             float(softmax_scale), float(p_dropout), seed, offset, offset_dev or 0,
-            1 if is_causal else 0, dt, rot_cos, rot_sin, rot_stride)
+            1 if is_causal else 0, dt, rot_cos, rot_sin, rot_stride, int(impl), 0)
         if layout is None:
             rc = raw_fwd(addr, _stream_ptr(dev))
         else:

@@ -20,6 +20,8 @@
  *   fa_index_add_first_axis <- IndexFirstAxisResidual.backward (flash_attn/bert_padding.py:82-94)
  *   fa_rotary               <- apply_rotary_pos_emb + RotaryEmbedding(2D).forward and their autograd
  *                              backward (flash_attn/rotary.py:22-41, 86-135)
+ *   (fa_fwd's D=64 non-causal shapes run a hand-scheduled gfx950 assembly kernel, csrc/asm/gen_fwd.py,
+ *    embedded in the library as a code object; FaFwdArgs.impl selects it or the HIP kernels)
  *   fa_query, fa_last_error, fa_version: host helpers (no reference counterpart; the reference
  *                                                  raised through TORCH_CHECK / exit(1),
  *                                                  fmha_api.cpp:131-170, fmha_utils.h:36-48)
@@ -97,7 +99,15 @@ typedef struct FaFwdArgs {
     const void *rot_cos;
     const void *rot_sin;
     int64_t rot_stride;
+    /* Kernel family (FA_IMPL_*). FA_IMPL_AUTO picks the fastest kernel for the shape: the
+     * hand-scheduled assembly forward for head_dim in (32, 64], non-causal, no dropout, dense,
+     * no fused rotary; the HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels (tests
+     * compare both; results agree within fp32 rounding of the row sums). */
+    int32_t impl;
+    int32_t reserved;         /* 0 */
 } FaFwdArgs;
+
+enum { FA_IMPL_AUTO = 0, FA_IMPL_HIP = 1 };
 
 /* Backward arguments. Mirrors the bwd call made by flash_attn_interface.py:31-33:
  * bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_q, cu_k, max_q, max_k, p, scale,

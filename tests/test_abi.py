@@ -84,8 +84,8 @@ def _valid_bwd_args(hip):
         setattr(a, f + "_row_stride", 256)
         setattr(a, f + "_head_stride", 128)
     a.batch, a.nheads, a.head_dim = 1, 2, 128
-    a.max_seqlen_q = 0                      # no query rows: returns before any launch
-    a.max_seqlen_k = 16
+    a.max_seqlen_q = 0                      # no query rows and no keys: returns before any launch
+    a.max_seqlen_k = 0                      # (with keys, dk/dv are zeroed: a launch, GPU tests)
     a.lse_stride = 16
     a.softmax_scale = 0.125
     a.dtype = hip.FA_DTYPE_BF16
@@ -104,7 +104,9 @@ def test_bwd_workspace_query_and_validation():
     assert L.fa_bwd(ctypes.byref(a), None) == 0          # max_seqlen_q = 0: nothing to launch (no grid 0)
     a.head_dim = 64
     a.max_seqlen_q = 4
-    assert L.fa_bwd(ctypes.byref(a), None) == 1          # D=64 with query rows needs dq_accum
+    a.max_seqlen_k = 16
+    assert L.fa_bwd(ctypes.byref(a), None) == 1          # D=64 with query rows and keys needs dq_accum
+    a.max_seqlen_k = 0
     a.max_seqlen_q = 0
     assert L.fa_bwd(ctypes.byref(a), None) == 0          # ... but not without any
     a.dq_accum = 4096

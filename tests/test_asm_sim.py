@@ -1,0 +1,105 @@
+"""CPU check of the hand-scheduled assembly forward (csrc/asm/gen_fwd.py) in the functional
+simulator tools/asm_sim.py: the generated instruction stream, run one workgroup at a time with
+the MFMA / LDS fragment maps of the MI355X guide, must reproduce the fp32 oracle
+(oracle/attention_ref.py, restating tests/test_flash_attn.py:115-159 of the reference) on small
+var-len cases, including the masked last tile, empty key sets and the rescale path. The GPU tests
+(tests/test_flash_attn.py, -m gpu) run the same kernel on the hardware."""
+import math
+import os
+import struct
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "hazyresearch_flash-attention_amd", "csrc", "asm"))
+
+import asm_sim  # noqa: E402
+import gen_fwd  # noqa: E402
+from oracle.attention_ref import attention_ref  # noqa: E402
+
+_TXT = {}
+
+
+def _kernel(dtype):
+    if dtype not in _TXT:
+        g = gen_fwd.Gen(dtype)
+        blocks, _ = gen_fwd.build(g)
+        _TXT[dtype] = gen_fwd.emit(g, blocks)
+    return _TXT[dtype]
+
+
+def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0):
+    rng = np.random.default_rng(seed)
+    cv = asm_sim.bf16_bits if dtype == "bf16" else asm_sim.f16_bits
+    B, tq, tk = len(lens_q), sum(lens_q), sum(lens_k)
+    q = cv(rng.standard_normal((tq, H, D)).astype(np.float32)).astype(np.uint16)
+    k = cv(rng.standard_normal((tk, H, D)).astype(np.float32)).astype(np.uint16)
+    v = cv(rng.standard_normal((tk, H, D)).astype(np.float32)).astype(np.uint16)
+    mem = asm_sim.Memory()
+    pq, pk, pv = mem.alloc(q), mem.alloc(k), mem.alloc(v)
+    po = mem.alloc(np.zeros((tq, H, D), np.uint16))
+    maxq = max(lens_q)
+    lse_stride = max((maxq + 15) // 16 * 16, 16)
+    pl = mem.alloc(np.full((B, H, lse_stride), 7.0, np.float32))
+    cq = np.concatenate([[0], np.cumsum(lens_q)]).astype(np.int32)
+    ck = np.concatenate([[0], np.cumsum(lens_k)]).astype(np.int32)
+    pcq, pck = mem.alloc(cq), mem.alloc(ck)
+    scale = D ** -0.5 if scale is None else scale
+    c = np.float32(scale * 1.4426950408889634)
+    nqb = (maxq + 255) // 256
+    mg = lambda d: ((1 << 32) + 2 * d - 1) // (2 * d)
+    karg = struct.pack("<7Q4Q4I2I2f2I2I2I", pq, pk, pv, po, pl, pcq, pck, D * 2, D * 2, D * 2, D * 2,
+                       H * D * 2, H * D * 2, H * D * 2, H * D * 2, H, lse_stride * 4, c, np.float32(8.0 / c),
+                       nqb, nqb * H * B, mg(nqb), mg(H), D, 0)
+    pa = mem.alloc(np.frombuffer(karg, np.uint8))
+    asm_sim.Sim(_kernel(dtype), dtype).run((nqb, H, B), pa, mem)
+    o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
+    lse = mem.get(pl).view(np.float32).reshape(B, H, lse_stride)
+    to = lambda x: torch.from_numpy(asm_sim.from16(x.astype(np.uint32), dtype))
+    qf, kf, vf = to(q), to(k), to(v)
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float16
+    for b in range(B):
+        sq, sk = slice(cq[b], cq[b + 1]), slice(ck[b], ck[b + 1])
+        o_b = torch.from_numpy(o[sq])
+        if lens_k[b] == 0:
+            assert torch.count_nonzero(o_b) == 0
+            assert np.all(lse[b, :, :lens_q[b]] == -np.inf)
+            continue
+        # the reference's own oracle at fp32 and at the input precision (the 2x rule of
+        # tests/test_flash_attn.py:407-409)
+        args = (qf[sq][None], kf[sk][None], vf[sk][None])
+        ref = attention_ref(*args, upcast=True)[0][0] if scale == D ** -0.5 else None
+        if ref is None:
+            s = torch.einsum("qhd,khd->hqk", qf[sq].double(), kf[sk].double()) * scale
+            ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), vf[sk].double()).float()
+            base = 4e-3
+        else:
+            lo = attention_ref(*(x.to(tdt) for x in args), upcast=False)[0][0].float()
+            base = (lo - ref).abs().max().item()
+        assert (o_b - ref).abs().max().item() <= 2 * base + 1e-4, (b, (o_b - ref).abs().max().item(), base)
+        s = torch.einsum("qhd,khd->hqk", qf[sq].double(), kf[sk].double()) * scale
+        ref_lse = torch.logsumexp(s, -1).numpy()
+        # the row sums cover the 16-bit-rounded P (what multiplies V): up to 2^-8 relative in the
+        # sum, so the LSE is within 4e-3
+        assert np.abs(lse[b, :, :lens_q[b]] - ref_lse).max() < 4e-3
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("lens_q,lens_k,H,D", [
+    ([130], [200], 1, 64),            # 3 full tiles + a masked one, rows past the block end
+    ([257, 40], [33, 190], 2, 64),    # var-len, two q-blocks, single masked tile
+    ([70], [700], 1, 64),             # 11 tiles: every unrolled loop position and its last-tile exit
+    ([40, 64], [0, 65], 1, 48),       # empty key set (zeros, -inf), head_dim < 64 zero-padded
+])
+def test_asm_forward_in_simulator(lens_q, lens_k, H, D, dtype):
+    _run(lens_q, lens_k, H, D, dtype)
+
+
+def test_asm_forward_rescale_path_in_simulator():
+    """A large softmax scale makes later tiles pass the running max by more than 2^8: the
+    out-of-line rescale block (O, row sums and the permuted alpha) runs past tile 0."""
+    _run([70], [300], 1, 64, "bf16", scale=3.0)

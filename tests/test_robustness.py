@@ -73,6 +73,26 @@ def test_backward_with_no_query_rows():
     assert out.shape == (0, H, d)
     dq, dk, dv = torch.autograd.grad(out, (q, k, v), torch.empty_like(out), allow_unused=True)
     assert dq.shape == q.shape
+    # no output depends on k or v: their gradients are zero, not uninitialised memory
+    assert dk is not None and dv is not None
+    assert torch.count_nonzero(dk).item() == 0 and torch.count_nonzero(dv).item() == 0
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_backward_with_no_keys(d):
+    """max_seqlen_k = 0 (every key set empty): the output is 0, dq = 0 and softmax_d = 0; at
+    D = 128 (dq written directly) no fp32 workspace is needed for that."""
+    fi = _fi()
+    H = 2
+    q = torch.randn(6, H, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.empty(0, H, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.empty(0, H, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    cu_q = torch.tensor([0, 6], dtype=torch.int32, device=DEV)
+    cu_k = torch.tensor([0, 0], dtype=torch.int32, device=DEV)
+    out = fi.flash_attn_unpadded_func(q, k, v, cu_q, cu_k, 6, 0, 0.0)
+    assert torch.count_nonzero(out).item() == 0
+    dq, = torch.autograd.grad(out, (q,), torch.randn_like(out))
+    assert torch.count_nonzero(dq).item() == 0
 
 
 def test_dropout_under_graph_capture_advances_the_stream():
