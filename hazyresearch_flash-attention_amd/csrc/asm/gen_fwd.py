@@ -52,8 +52,24 @@ TILE = BN * D * 2      # bytes per tile image
 KREG = 0
 VREG = R * TILE
 LDS_BYTES = 2 * R * TILE
+VREADS_P1 = False      # V^T fragment reads of tile j in phase 1 (one phase ahead of PV_A(j))
+SM_PIPE = False        # software-pipelined fma -> exp -> cvt order inside the softmax
+DMA_P2 = False         # all four DMA pieces of a tile in phase 2 (K's with V's)
+SPEC = True            # exps against the current max; rescale test branches at the phase end
+
+
+def set_geometry(r, dist):
+    """Ring of r slots per tensor, DMA distance dist (<= r - 1: a slot is rewritten only after
+    the barrier that follows its last read); the loop unroll is lcm(r, 2)."""
+    global R, DIST, U, VREG, LDS_BYTES
+    assert 1 <= dist <= r - 1
+    R, DIST = r, dist
+    U = r * 2 // math.gcd(r, 2)
+    VREG = R * TILE
+    LDS_BYTES = 2 * R * TILE
 RESCALE_THR = 8.0      # log2-domain threshold of the deferred rescale (fa_fwd_kernel.h)
 OOB = 0x80000000
+PROBE = set()          # timing-only variants (tools/asm_variants.py); empty in the product build
 
 # ---- VGPRs (arch)
 V_KADDR = 4            # 4: K fragment read address per k-step
@@ -72,7 +88,8 @@ V_OOFF = {'A': 136, 'B': 140}   # 4 each: O store offsets (dt, g)
 V_LOFF = {'A': 144, 'B': 145}   # LSE store offset
 V_ONEF = 146           # 1.0f
 V_LANE = 147
-NVGPR = 148
+V_ETMP = 148           # 16: rotating exp temporaries of the speculative softmax (S stays intact)
+NVGPR = 164
 # ---- AGPRs
 A_O = {'A': 0, 'B': 32}         # O^T accumulators (2 d-blocks x 16)
 A_L = {'A': 64, 'B': 68}        # row-sum accumulators (16x16 MFMA C)
@@ -84,6 +101,7 @@ NAGPR = 236
 
 # ---- SGPRs
 S_KD, S_VD, S_QD, S_OD, S_LD = 8, 12, 16, 20, 24   # buffer descriptors (4 each)
+S_KD1, S_VD1 = 80, 84  # second K / V descriptor sets (odd tiles; prologue temporaries before)
 S_C, S_THR, S_J, S_NT, S_LAST = 28, 29, 30, 31, 32
 S_KSTEP, S_VSTEP, S_WAVE = 35, 36, 37
 S_M0B = 38             # 1024 * wave: this wave's DMA pieces start at piece `wave`
@@ -199,7 +217,7 @@ class Gen:
                     use[f] = len(out)
                     out.append(Inst(f'{self.mf32} {as_(acc, 16)}, {as_(vf, 4)}, {vs(p, 4)}, {as_(acc, 16)}', 'mfma', 8,
                                     rd=ra(vf, 4) + rv(p, 4), wr=ra(acc, 16), rdc=ra(acc, 16), pipe=32))
-                if si < 4:
+                if si < 4 and 'nosum' not in PROBE:
                     out.append(sums[si])
                     si += 1
         return out, use
@@ -208,6 +226,8 @@ class Gen:
     def kreads(self, t):
         """K(t) fragments from ring slot t % R into buffer t % 2 (8 x ds_read_b128)."""
         out = []
+        if 'nolds' in PROBE:
+            return out
         slot = KREG + (t % R) * TILE
         for st in range(2):
             for ks in range(4):
@@ -220,6 +240,8 @@ class Gen:
         """V(t)^T fragments from ring slot t % R into buffer t % 2 (16 x ds_read_b64_tr_b16).
         Returns list of (frag, inst)."""
         out = []
+        if 'nolds' in PROBE:
+            return out
         slot = VREG + (t % R) * TILE
         for dt in range(2):
             for st in range(2):
@@ -228,36 +250,118 @@ class Gen:
                     vf = A_VF + 32 * (t % 2) + 4 * f
                     for half in range(2):
                         addr = V_VADDR + dt * 2 + half
-                        off = slot + (32 * st + 16 * s) * 128
+                        off = slot - VREG + (32 * st + 16 * s) * 128   # VREG is in the address VGPR
                         out.append((f, Inst(f'ds_read_b64_tr_b16 {as_(vf + 2 * half, 2)}, v{addr} offset:{off}', 'ds', 2,
                                             rd=[f'v{addr}'], wr=ra(vf + 2 * half, 2))))
         return out
 
     def dma(self, kind, t):
+        if 'nodma' in PROBE:
+            return []
+        return self._dma(kind, t)
+
+    def _dma(self, kind, t):
         """This wave's two 1-KiB pieces of the K or V tile t (LDS-DMA into ring slot t % R).
-        The descriptor walks the sequence: after each tile its base advances by 64 rows and
-        num_records shrinks by the same bytes, saturating at 0, so rows past the end (and every
-        tile past the last) read as zeros whatever the SGPR-offset range-check rule is."""
+        Tile t reads through descriptor set t % 2. Each set walks the sequence two tiles at a
+        time: right before its next use its base advances by 128 rows and num_records shrinks by
+        the same bytes, saturating at 0, so rows past the end (and every tile past the last) read
+        as zeros whatever the SGPR-offset range-check rule is. Updating the set used two tiles
+        ago (not the one a DMA just read) keeps the SALU writes off SGPRs an in-flight LDS-DMA
+        still reads (measured -4 % against a walk right behind the DMA)."""
         out = []
         region = KREG if kind == 'K' else VREG
-        desc = S_KD if kind == 'K' else S_VD
-        step = S_KSTEP if kind == 'K' else S_VSTEP
+        desc = (S_KD if t % 2 == 0 else S_KD1) if kind == 'K' else (S_VD if t % 2 == 0 else S_VD1)
+        step = S_KSTEP if kind == 'K' else S_VSTEP          # 2 tiles of bytes
         dregs = [f's{desc + i}' for i in range(4)]
+        if t >= 2 and 'nowalk' not in PROBE:
+            st = f's{step}'
+            out.append(salu(f's_add_u32 s{desc}, s{desc}, {st}', rd=[dregs[0], st], wr=[dregs[0], 'scc']))
+            out.append(salu(f's_addc_u32 s{desc + 1}, s{desc + 1}, 0', rd=[dregs[1], 'scc'], wr=[dregs[1], 'scc']))
+            out.append(salu(f's_sub_u32 s{desc + 2}, s{desc + 2}, {st}', rd=[dregs[2], st], wr=[dregs[2], 'scc']))
+            out.append(salu(f's_cselect_b32 s{desc + 2}, 0, s{desc + 2}', rd=[dregs[2], 'scc'], wr=[dregs[2]]))
         for i in range(2):
             m0 = region + (t % R) * TILE + 4096 * i   # + 1024 * wave (S_M0B)
             voff = V_DMA + (0 if kind == 'K' else 2) + i
             out.append(Inst(f's_add_u32 m0, s{S_M0B}, {m0}', 'm0', 2, rd=[f's{S_M0B}'], wr=['m0', 'scc']))
             out.append(Inst(f'buffer_load_dwordx4 v{voff}, s[{desc}:{desc + 3}], 0 offen lds', 'dma', 16,
                             rd=[f'v{voff}', 'm0'] + dregs))
-        st = f's{step}'
-        out.append(salu(f's_add_u32 s{desc}, s{desc}, {st}', rd=[dregs[0], st], wr=[dregs[0], 'scc']))
-        out.append(salu(f's_addc_u32 s{desc + 1}, s{desc + 1}, 0', rd=[dregs[1], 'scc'], wr=[dregs[1], 'scc']))
-        out.append(salu(f's_sub_u32 s{desc + 2}, s{desc + 2}, {st}', rd=[dregs[2], st], wr=[dregs[2], 'scc']))
-        out.append(salu(f's_cselect_b32 s{desc + 2}, 0, s{desc + 2}', rd=[dregs[2], 'scc'], wr=[dregs[2]]))
         return out
 
     # ------------------------------------------------------------------ softmax of one tile
+    def exp_stream(self, X, mc):
+        """P_X = cvt(exp2(S_X c - mc)) through the 16 rotating temporaries: fma(i) at step i,
+        exp(i) at step i + 4, cvt of pair q at step 2q + 9 (every consumer 4+ instructions
+        behind its producer; temporary i % 16 is free again before element i + 16 needs it)."""
+        S, P, E = V_S[X], V_P[X], V_ETMP
+        steps = []
+        for i in range(32):
+            e = E + i % 16
+            steps.append((i, 0, Inst(f'v_fma_f32 v{e}, v{S + i}, s{S_C}, -v{mc}', 'valu', 4,
+                                     rd=[f'v{S + i}', f's{S_C}', f'v{mc}'], wr=[f'v{e}'])))
+            steps.append((i + 4, 1, V(f'v_exp_f32 v{e}, v{e}', e, [e], kind='trans', cost=8)))
+        for q in range(16):
+            a, b = E + (2 * q) % 16, E + (2 * q + 1) % 16
+            steps.append((2 * q + 9, 2, V(f'{self.cvt} v{P + q}, v{a}, v{b}', P + q, [a, b])))
+        return [x for _, _, x in sorted(steps, key=lambda z: (z[0], z[1]))]
+
+    def max_ops(self, X):
+        """Row max of S_X (4 v_max3 chains, merge, lane pair (l, l^32)) and the rescale test
+        (vcc = lanes whose tile max passed the threshold)."""
+        S, T, mthr = V_S[X], V_TMP[X], V_MTHR[X]
+        chains = []
+        for k in range(4):
+            c = [S + 8 * k + e for e in range(8)]
+            t = T + k
+            chains.append([V(f'v_max3_f32 v{t}, v{c[0]}, v{c[1]}, v{c[2]}', t, c[0:3]),
+                           V(f'v_max3_f32 v{t}, v{t}, v{c[3]}, v{c[4]}', t, [t, c[3], c[4]]),
+                           V(f'v_max3_f32 v{t}, v{t}, v{c[5]}, v{c[6]}', t, [t, c[5], c[6]]),
+                           V(f'v_max_f32 v{t}, v{t}, v{c[7]}', t, [t, c[7]])])
+        out = [chains[k][st] for st in range(4) for k in range(4)]
+        out += [V(f'v_max3_f32 v{T + 4}, v{T}, v{T + 1}, v{T + 2}', T + 4, [T, T + 1, T + 2]),
+                V(f'v_max_f32 v{T + 4}, v{T + 4}, v{T + 3}', T + 4, [T + 4, T + 3]),
+                V(f'v_mov_b32 v{T + 5}, v{T + 4}', T + 5, [T + 4]),
+                Inst(f'v_permlane32_swap_b32 v{T + 4}, v{T + 5}', 'perm', 4,
+                     rd=[f'v{T + 4}', f'v{T + 5}'], wr=[f'v{T + 4}', f'v{T + 5}']),
+                V(f'v_max_f32 v{T + 6}, v{T + 4}, v{T + 5}', T + 6, [T + 4, T + 5]),
+                V(f'v_cmp_gt_f32 vcc, v{T + 6}, v{mthr}', 'vcc', [T + 6, mthr])]
+        return out
+
+    def softmax_spec(self, X, masked, rescue):
+        """Speculative form: the exps run against the current m while the max tree runs
+        beside them (no dependence between the two), and the rescale test branches only at the
+        end of the phase, when its vcc is long known; the rare rescale block then moves m,
+        scales O and the row sums and recomputes P from the untouched S."""
+        S, P, T = V_S[X], V_P[X], V_TMP[X]
+        mthr, mc = V_MTHR[X], V_MC[X]
+        out = []
+        if masked:
+            for i in range(32):
+                st, r = divmod(i, 16)
+                kofs = 32 * st + (r & 3) + 8 * (r >> 2)
+                out.append(V(f'v_cmp_lt_i32 vcc, {kofs}, v{V_NVREL}', 'vcc', [V_NVREL]))
+                out.append(Inst(f'v_cndmask_b32 v{S + i}, v{V_NEGINF}, v{S + i}, vcc', 'valu', 4,
+                                rd=[f'v{V_NEGINF}', f'v{S + i}', 'vcc'], wr=[f'v{S + i}']))
+        ex = self.exp_stream(X, mc)
+        mx = self.max_ops(X)
+        # max ops spread over the first 70 % of the exp stream
+        out += merge(ex, [(i, x) for i, x in zip(spread(len(mx), 2, int(len(ex) * 0.7)), mx)])
+        resc, ret = self.lab(f'resc{X}'), self.lab(f'ret{X}')
+        touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], 32) + ra(A_L[X], 4) + rv(V_ETMP, 16) + rv(P, 16)
+        out.append(Inst(f's_cbranch_vccnz {resc}\n{ret}:', 'br', 4, rd=['vcc'] + touched, wr=touched))
+        rb = self.rescale_block(X, resc, ret)
+        rb[-2:-2] = self.exp_stream(X, mc)       # recompute P with the new m (before the s_nop 2)
+        rescue.append(rb)
+        if 'nofill' in PROBE:
+            out = []
+            rescue.pop()
+        return out
+
     def softmax(self, X, masked, rescue):
+        if SPEC:
+            return self.softmax_spec(X, masked, rescue)
+        return self.softmax_serial(X, masked, rescue)
+
+    def softmax_serial(self, X, masked, rescue):
         """Block X's softmax of the tile in S_X: [mask], max tree, deferred-rescale test
         (branch to an out-of-line block), exp2(s c - m c), conversion into P_X.
         rescue: list that receives the out-of-line rescale block."""
@@ -283,6 +387,8 @@ class Gen:
         for step in range(4):
             for k in range(4):
                 out.append(chains[k][step])
+        if 'nomax' in PROBE:
+            out = [x for x in out if not x.txt.startswith(('v_max', 'v_cmp_lt'))]
         out.append(V(f'v_max3_f32 v{T + 4}, v{T}, v{T + 1}, v{T + 2}', T + 4, [T, T + 1, T + 2]))
         out.append(V(f'v_max_f32 v{T + 4}, v{T + 4}, v{T + 3}', T + 4, [T + 4, T + 3]))
         out.append(V(f'v_mov_b32 v{T + 5}, v{T + 4}', T + 5, [T + 4]))
@@ -290,6 +396,10 @@ class Gen:
                         rd=[f'v{T + 4}', f'v{T + 5}'], wr=[f'v{T + 4}', f'v{T + 5}']))
         out.append(V(f'v_max_f32 v{T + 6}, v{T + 4}, v{T + 5}', T + 6, [T + 4, T + 5]))
         out.append(V(f'v_cmp_gt_f32 vcc, v{T + 6}, v{mthr}', 'vcc', [T + 6, mthr]))
+        if 'nomax' in PROBE:
+            out += [V(f'v_max_f32 v{T + 6}, v{S}, v{S + 1}', T + 6, [S, S + 1]),
+                    V(f'v_cmp_gt_f32 vcc, v{T + 6}, v{mthr}', 'vcc', [T + 6, mthr])]
+            out = [x for x in out if not (x.txt.startswith('v_cmp_gt_f32') and x is not out[-1])]
         resc, ret = self.lab(f'resc{X}'), self.lab(f'ret{X}')
         # branch and its return label form one unbreakable group
         # (it also carries the registers the out-of-line block touches, so the scheduler keeps
@@ -298,7 +408,20 @@ class Gen:
         out.append(Inst(f's_cbranch_vccnz {resc}\n{ret}:', 'br', 4, rd=['vcc'] + touched, wr=touched))
         rescue.append(self.rescale_block(X, resc, ret))
         # exp2(s * c - m * c), converted pairwise into the 16-bit P operand
-        for q in range(16):
+        if SM_PIPE:
+            # fma(i) at step i, exp(i) at step i + 4, cvt of pair q at step 2q + 9: every
+            # dependent instruction sits 4+ instructions behind its producer
+            steps = []
+            for i in range(32):
+                a = S + i
+                steps.append((i, 0, Inst(f'v_fma_f32 v{a}, v{a}, s{S_C}, -v{mc}', 'valu', 4,
+                                         rd=[f'v{a}', f's{S_C}', f'v{mc}'], wr=[f'v{a}'])))
+                steps.append((i + 4, 1, V(f'v_exp_f32 v{a}, v{a}', a, [a], kind='trans', cost=8)))
+            for q in range(16):
+                steps.append((2 * q + 9, 2, V(f'{self.cvt} v{P + q}, v{S + 2 * q}, v{S + 2 * q + 1}', P + q,
+                                              [S + 2 * q, S + 2 * q + 1])))
+            out += [x for _, _, x in sorted(steps, key=lambda z: (z[0], z[1]))]
+        for q in ([] if SM_PIPE else range(16)):
             a, b = S + 2 * q, S + 2 * q + 1
             out.append(Inst(f'v_fma_f32 v{a}, v{a}, s{S_C}, -v{mc}', 'valu', 4, rd=[f'v{a}', f's{S_C}', f'v{mc}'],
                             wr=[f'v{a}']))
@@ -309,7 +432,20 @@ class Gen:
             if q >= 1:
                 out.append(V(f'{self.cvt} v{P + q - 1}, v{S + 2 * q - 2}, v{S + 2 * q - 1}', P + q - 1,
                              [S + 2 * q - 2, S + 2 * q - 1]))
-        out.append(V(f'{self.cvt} v{P + 15}, v{S + 30}, v{S + 31}', P + 15, [S + 30, S + 31]))
+        if not SM_PIPE:
+            out.append(V(f'{self.cvt} v{P + 15}, v{S + 30}, v{S + 31}', P + 15, [S + 30, S + 31]))
+        if 'expmov' in PROBE:     # price the transcendental beyond a plain VALU op
+            for x in out:
+                if x.txt.startswith('v_exp_f32'):
+                    x.txt = x.txt.replace('v_exp_f32', 'v_mov_b32')
+                    x.kind, x.cost = 'valu', 4
+        drop = {'noexp': 'v_exp', 'nofma': 'v_fma', 'nocvt': 'v_cvt'}
+        for k, pre in drop.items():
+            if k in PROBE:
+                out = [x for x in out if not x.txt.startswith(pre)]
+        if 'nofill' in PROBE:
+            out = []
+            rescue.pop()
         return out
 
     def rescale_block(self, X, resc, ret):
@@ -396,8 +532,10 @@ class Gen:
         mf = self.qk('B', t) + self.pv_sum('B', t - 1)[0]
         sm = self.softmax('A', masked, rescue)
         side = [] if last else self.kreads(t + 1)
-        dma = [] if last else self.dma('K', t + 1 + DIST)
-        fill = merge(sm, [(i, x) for i, x in zip(spread(len(side), 27, len(sm) - 4), side)] +
+        if VREADS_P1:
+            side = [x for _, x in self.vreads(t)] + side
+        dma = [] if (last or DMA_P2) else self.dma('K', t + 1 + DIST)
+        fill = merge(sm, [(i, x) for i, x in zip(spread(len(side), 16, len(sm) - 4), side)] +
                      [(i, x) for i, x in zip(spread(len(dma), 6, len(sm) - 10), dma)])
         return [mark()] + place(mf, fill)
 
@@ -409,10 +547,12 @@ class Gen:
         mf = qk + pv
         sm = self.softmax('B', masked, rescue)
         vr = []
-        for f, ins in self.vreads(t):
+        for f, ins in ([] if VREADS_P1 else self.vreads(t)):
             ins.deadline = max(0, len(qk) + use[f] - 3)
             vr.append(ins)
         dma = [] if last else self.dma('V', t + DIST)
+        if DMA_P2 and not last:
+            dma = self.dma('K', t + 1 + DIST) + dma
         # the V reads go early (two per softmax instruction pair), the DMA pieces in the middle
         fill = merge(sm, [(i, x) for i, x in zip(spread(len(vr), 1, 56), vr)] +
                      [(i, x) for i, x in zip(spread(len(dma), 30, len(sm) - 10), dma)])
@@ -447,6 +587,8 @@ def merge(base, extra):
 
 
 def place(mfmas, fillers, window=10):
+    if 'nomfma' in PROBE:
+        mfmas = []
     """Distribute the filler sequence over the gaps after each MFMA in proportion to the MFMA
     pipe cycles; a filler with a deadline k is issued before MFMA k. Within that, a small list
     scheduler may issue a later independent filler first when the next one would need wait
@@ -779,8 +921,14 @@ def prologue(g):
     p += [S(f's_mov_b32 s{S_C}, s68'), S(f's_mov_b32 s{S_THR}, s69'),
           S(f's_add_u32 s{S_NT}, s79, 63'), S(f's_lshr_b32 s{S_NT}, s{S_NT}, 6'),
           S(f's_sub_u32 s{S_LAST}, s{S_NT}, 1'), S(f's_mov_b32 s{S_J}, 0'),
-          S(f's_lshl_b32 s{S_KSTEP}, s63, 6'), S(f's_lshl_b32 s{S_VSTEP}, s64, 6'),
+          S(f's_lshl_b32 s{S_KSTEP}, s63, 7'), S(f's_lshl_b32 s{S_VSTEP}, s64, 7'),
           S(f's_lshl_b32 s{S_M0B}, s{S_WAVE}, 10')]
+    # second descriptor sets (odd tiles): one tile (64 rows) further, num_records saturating
+    for d0, d1, rs in ((S_KD, S_KD1, 63), (S_VD, S_VD1, 64)):
+        p += [S(f's_lshl_b32 s96, s{rs}, 6'),
+              S(f's_add_u32 s{d1}, s{d0}, s96'), S(f's_addc_u32 s{d1 + 1}, s{d0 + 1}, 0'),
+              S(f's_sub_u32 s{d1 + 2}, s{d0 + 2}, s96'), S(f's_cselect_b32 s{d1 + 2}, 0, s{d1 + 2}'),
+              S(f's_mov_b32 s{d1 + 3}, s{d0 + 3}')]
     # ---- per-lane constants
     L = V_LANE
     p += [V(f'v_and_b32 v{L}, 63, v0', L, [0]), V('v_and_b32 v16, 31, v0', 16, [0]),
@@ -799,7 +947,9 @@ def prologue(g):
         for dt in range(2):
             p += [V(f'v_add_u32 v29, {4 * dt}, v25', 29, [25]), V('v_xor_b32 v29, v29, v28', 29, [29, 28]),
                   V('v_lshl_or_b32 v29, v29, 4, v26', 29, [29, 26]),
-                  V(f'v_lshl_add_u32 v{V_VADDR + dt * 2 + half}, v27, 7, v29', V_VADDR + dt * 2 + half, [27, 29])]
+                  V(f'v_lshl_add_u32 v{V_VADDR + dt * 2 + half}, v27, 7, v29', V_VADDR + dt * 2 + half, [27, 29]),
+                  V(f'v_add_u32 v{V_VADDR + dt * 2 + half}, {VREG}, v{V_VADDR + dt * 2 + half}',
+                    V_VADDR + dt * 2 + half, [V_VADDR + dt * 2 + half])]
     p += [V(f'v_mov_b32 v{V_NEGINF}, 0xff800000', V_NEGINF, []), V(f'v_mov_b32 v{V_ONEF}, 1.0', V_ONEF, []),
           V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
     # DMA source offsets: pieces `wave` and `wave + 4` of a tile; lane l -> row 8p + l/8, slot l%8
@@ -865,7 +1015,7 @@ def prologue(g):
     p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in (V_MTHR['A'], V_MTHR['B'], V_MC['A'], V_MC['B'])]
     p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
-    p += [raw('s_waitcnt vmcnt(8)'), raw('s_barrier')]
+    p += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier')]
     # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
     p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
     p += [raw('s_nop 7'), raw('s_nop 3')]
@@ -912,8 +1062,8 @@ def last_tile(g, t, rescue):
     next-tile reads or DMA, then P.V of block B and the two epilogues."""
     b = [label(f'.Llast{t}')]
     tmp = V_TMP['A'] + 7
-    b += [S(f's_lshl_b32 s80, s{S_J}, 6'), S('s_sub_u32 s80, s79, s80'),
-          V(f'v_mov_b32 v{V_NVREL}, s80', V_NVREL, []),
+    b += [S(f's_lshl_b32 s96, s{S_J}, 6'), S('s_sub_u32 s96, s79, s96'),
+          V(f'v_mov_b32 v{V_NVREL}, s96', V_NVREL, []),
           V(f'v_bfe_u32 v{tmp}, v{V_LANE}, 5, 1', tmp, [V_LANE]),
           V(f'v_lshlrev_b32 v{tmp}, 2, v{tmp}', tmp, [tmp]),
           V(f'v_sub_u32 v{V_NVREL}, v{V_NVREL}, v{tmp}', V_NVREL, [V_NVREL, tmp])]
@@ -943,7 +1093,9 @@ def build(g):
         blk += g.phase2(t, rescue=rescue)
         if DUMP and DUMP[0] == 'p2' and t == 0:
             blk += dump_block(DUMP[1])
-        blk += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier'), S(f's_add_u32 s{S_J}, s{S_J}, 1')]
+        if 'nobar' not in PROBE:
+            blk += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier')]
+        blk += [S(f's_add_u32 s{S_J}, s{S_J}, 1')]
         if t == U - 1:
             blk.append(raw('s_branch .Lloop'))
         tiles.append(blk)
@@ -976,6 +1128,11 @@ def build(g):
 
 def emit(g, blocks):
     name = g.name
+    if 'nolgkm' in PROBE or 'novm' in PROBE:
+        for blk in blocks[1:]:
+            blk[:] = [x for x in blk if not (x.txt.startswith('s_waitcnt') and
+                                             (('nolgkm' in PROBE and 'lgkmcnt' in x.txt) or
+                                              ('novm' in PROBE and 'vmcnt' in x.txt and 'lgkm' not in x.txt)))]
     lines = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', '.amdhsa_code_object_version 5', '.text',
              f'.globl {name}', '.p2align 8', f'.type {name},@function', f'{name}:']
     for blk in blocks:
@@ -1042,11 +1199,31 @@ def main():
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats', action='store_true')
     ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')
+    ap.add_argument('--probe', default='', help='timing-only variant switches, comma separated')
+    ap.add_argument('--ring', type=int, default=None)
+    ap.add_argument('--dist', type=int, default=None)
+    ap.add_argument('--vp1', type=int, default=None)
+    ap.add_argument('--smpipe', type=int, default=None)
+    ap.add_argument('--dmap2', type=int, default=None)
+    ap.add_argument('--spec', type=int, default=None)
     args = ap.parse_args()
     global DUMP
     if args.dump:
         pt, regs = args.dump.split(':')
         DUMP = (pt, expand_regs(regs))
+    PROBE.update(x for x in args.probe.split(',') if x)
+    global VREADS_P1, SM_PIPE
+    if args.ring or args.dist:
+        set_geometry(args.ring or R, args.dist or DIST)
+    if args.vp1 is not None:
+        VREADS_P1 = bool(args.vp1)
+    if args.smpipe is not None:
+        SM_PIPE = bool(args.smpipe)
+    global DMA_P2, SPEC
+    if args.spec is not None:
+        SPEC = bool(args.spec)
+    if args.dmap2 is not None:
+        DMA_P2 = bool(args.dmap2)
     g = Gen(args.dtype)
     blocks, n = build(g)
     txt = emit(g, blocks)

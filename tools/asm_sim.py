@@ -535,8 +535,6 @@ class Sim:
         voff = self.vread(w, vo).astype(np.int64)
         soff = self.sread(w, so)
         n = {'buffer_load_dwordx4': 16, 'buffer_store_dwordx4': 16, 'buffer_store_dword': 4}[op]
-        if srd == 's[84:87]':   # debug dump descriptor (gen_fwd.py --dump): unbounded
-            nrec = 1 << 62
         chk = voff + off + (soff if self.soff_checked else 0)
         ok = (voff & 0x80000000) == 0
         ok &= chk + n <= nrec

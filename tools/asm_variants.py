@@ -1,0 +1,113 @@
+"""asm_variants.py — timing of assembly-forward variants (gen_fwd.py --probe switches) in one
+process, interleaved, at a BASELINE shape. Probe variants compute wrong results by design
+(a part is removed to price it); the base variant is the product kernel.
+
+    python tools/asm_variants.py [--shape B,H,S] [--variants ",nomax,noexp"] [--rounds 5]
+"""
+import argparse
+import ctypes
+import os
+import struct
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GEN = os.path.join(ROOT, "hazyresearch_flash-attention_amd", "csrc", "asm", "gen_fwd.py")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def build(spec, out_dir):
+    """spec: 'label:generator args' (e.g. 'vp1:--vp1 1 --probe noexp') or a bare probe switch."""
+    if ":" in spec:
+        tag, args = spec.split(":", 1)
+        extra = args.split()
+    else:
+        tag, extra = spec or "base", (["--probe", spec] if spec else [])
+    s = os.path.join(out_dir, f"var_{tag}.s")
+    subprocess.check_call([sys.executable, GEN, "--out", s] + list(extra))
+    subprocess.check_call([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
+                           s, "-o", s[:-2] + ".o"])
+    subprocess.check_call([f"{LLVM}/ld.lld", "-shared", s[:-2] + ".o", "-o", s[:-2] + ".hsaco"])
+    return open(s[:-2] + ".hsaco", "rb").read()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="8,12,2048")
+    ap.add_argument("--variants", default=",nomax,noexp,nofma,nocvt,nofill,nodma,nolds,nosum,nobar")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=50)
+    args = ap.parse_args()
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    # ';'-separated 'label:generator args' specs, or ','-separated probe switches ('' = base)
+    variants = args.variants.split(";") if ";" in args.variants else args.variants.split(",")
+    images = {v: build(v, out) for v in variants}
+    import torch
+    B, H, S = (int(x) for x in args.shape.split(","))
+    D = 64
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    q = torch.randn(B * S, H, D, generator=g).bfloat16().to(dev)
+    k = torch.randn(B * S, H, D, generator=g).bfloat16().to(dev)
+    v = torch.randn(B * S, H, D, generator=g).bfloat16().to(dev)
+    o = torch.empty_like(q)
+    lse_stride = (S + 15) // 16 * 16
+    lse = torch.empty(B, H, lse_stride, device=dev)
+    cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=dev)
+    nqb = (S + 255) // 256
+    mg = lambda d: ((1 << 32) + 2 * d - 1) // (2 * d)
+    c = np.float32(D ** -0.5 * 1.4426950408889634)
+    kb = struct.pack("<7Q4Q4I2I2f2I2I2I", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
+                     cu.data_ptr(), cu.data_ptr(), D * 2, D * 2, D * 2, D * 2, H * D * 2, H * D * 2, H * D * 2,
+                     H * D * 2, H, lse_stride * 4, c, np.float32(8.0 / c), nqb, nqb * H * B, mg(nqb), mg(H), D, 0)
+    libs = [ln.split()[-1] for ln in open("/proc/self/maps").read().split("\n") if "libamdhip64" in ln]
+    hip = ctypes.CDLL(libs[0])
+    kbuf = ctypes.create_string_buffer(kb, len(kb))
+    size = ctypes.c_size_t(len(kb))
+    extra = (ctypes.c_void_p * 5)(1, ctypes.addressof(kbuf), 2, ctypes.addressof(size), 3)
+    fns = {}
+    keep = []
+    for name, img in images.items():
+        mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(img, len(img))
+        keep.append(buf)
+        assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
+        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"fa_fwd_d64_bf16_asm") == 0
+        fns[name] = fn
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def launch(fn):
+        rc = hip.hipModuleLaunchKernel(fn, nqb, H, B, 256, 1, 1, 0, stream, None, extra)
+        assert rc == 0
+
+    flops = 4.0 * B * H * S * S * D
+    # warm the clock
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        for _ in range(20):
+            launch(fns[variants[0]])
+        torch.cuda.synchronize()
+    res = {n: [] for n in variants}
+    for _ in range(args.rounds):
+        for n in variants:
+            for _ in range(5):
+                launch(fns[n])
+            s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_.record()
+            for _ in range(args.iters):
+                launch(fns[n])
+            e_.record()
+            torch.cuda.synchronize()
+            res[n].append(s_.elapsed_time(e_) / args.iters)
+    base = np.median(res[variants[0]])
+    for n in variants:
+        m = float(np.median(res[n]))
+        print(f"{(n.split(':')[0] if n else 'base'):24s} {m * 1e3:8.2f} us  {flops / m / 1e9:7.1f} TF/s  {100 * (m / base - 1):+6.1f}%", flush=True)
+
+
+if __name__ == "__main__":
+    main()
