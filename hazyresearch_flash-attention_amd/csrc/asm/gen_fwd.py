@@ -56,6 +56,12 @@ VREADS_P1 = False      # V^T fragment reads of tile j in phase 1 (one phase ahea
 SM_PIPE = False        # software-pipelined fma -> exp -> cvt order inside the softmax
 DMA_P2 = False         # all four DMA pieces of a tile in phase 2 (K's with V's)
 SPEC = True            # exps against the current max; rescale test branches at the phase end
+ORDET = False          # rescale test = top exponent bit of the packed P (any P >= 2) by an OR tree;
+#                        the max tree moves into the out-of-line rescale block
+ORDET_DELTA = {'bf16': 8.0, 'f16': 2.0}   # a rescale sets m = tile max * c + delta (P <= 2^-delta)
+EXP_LAG = 4            # exp_stream: fma(i) -> exp(i) distance (instructions)
+CVT_LAG = 4            # exp_stream: exp -> cvt distance
+MC_BANKS = False       # fma reads m*c from one of 4 copies in a VGPR bank other than its S operand
 
 
 def set_geometry(r, dist):
@@ -89,6 +95,7 @@ V_LOFF = {'A': 144, 'B': 145}   # LSE store offset
 V_ONEF = 146           # 1.0f
 V_LANE = 147
 V_ETMP = 148           # 16: rotating exp temporaries of the speculative softmax (S stays intact)
+V_MCB = {'A': 164, 'B': 168}    # 4 each (MC_BANKS): copies of m*c in VGPR banks 0..3
 NVGPR = 164
 # ---- AGPRs
 A_O = {'A': 0, 'B': 32}         # O^T accumulators (2 d-blocks x 16)
@@ -288,20 +295,44 @@ class Gen:
         return out
 
     # ------------------------------------------------------------------ softmax of one tile
-    def exp_stream(self, X, mc):
+    def mc_reg(self, X, sreg, mc):
+        """The m*c register an fma with S operand v{sreg} reads: m*c itself, or with MC_BANKS
+        the copy two VGPR banks away from the S operand (no read-port conflict)."""
+        if not MC_BANKS:
+            return mc
+        return next(c for c in range(V_MCB[X], V_MCB[X] + 4) if c % 4 == (sreg % 4 + 2) % 4)
+
+    def exp_stream(self, X, mc, ortest=False):
         """P_X = cvt(exp2(S_X c - mc)) through the 16 rotating temporaries: fma(i) at step i,
-        exp(i) at step i + 4, cvt of pair q at step 2q + 9 (every consumer 4+ instructions
-        behind its producer; temporary i % 16 is free again before element i + 16 needs it)."""
+        exp(i) at step i + EXP_LAG, cvt of pair q at step 2q + 1 + EXP_LAG + CVT_LAG (every
+        consumer several instructions behind its producer; temporary i % 16 is free again before
+        element i + 16 needs it). ortest: also the ORDET rescale test over the packed P (an OR
+        chain behind the cvts, then vcc = lanes holding some P >= 2: bit 14 of either half is
+        the top exponent bit of a bf16 / f16 >= 2, and of inf / NaN)."""
         S, P, E = V_S[X], V_P[X], V_ETMP
+        assert EXP_LAG + CVT_LAG + 1 < 16
         steps = []
         for i in range(32):
             e = E + i % 16
-            steps.append((i, 0, Inst(f'v_fma_f32 v{e}, v{S + i}, s{S_C}, -v{mc}', 'valu', 4,
-                                     rd=[f'v{S + i}', f's{S_C}', f'v{mc}'], wr=[f'v{e}'])))
-            steps.append((i + 4, 1, V(f'v_exp_f32 v{e}, v{e}', e, [e], kind='trans', cost=8)))
+            m = self.mc_reg(X, S + i, mc)
+            steps.append((i, 0, Inst(f'v_fma_f32 v{e}, v{S + i}, s{S_C}, -v{m}', 'valu', 4,
+                                     rd=[f'v{S + i}', f's{S_C}', f'v{m}'], wr=[f'v{e}'])))
+            steps.append((i + EXP_LAG, 1, V(f'v_exp_f32 v{e}, v{e}', e, [e], kind='trans', cost=8)))
+        cvt_at = {}
         for q in range(16):
             a, b = E + (2 * q) % 16, E + (2 * q + 1) % 16
-            steps.append((2 * q + 9, 2, V(f'{self.cvt} v{P + q}, v{a}, v{b}', P + q, [a, b])))
+            cvt_at[q] = 2 * q + 1 + EXP_LAG + CVT_LAG
+            steps.append((cvt_at[q], 2, V(f'{self.cvt} v{P + q}, v{a}, v{b}', P + q, [a, b])))
+        if ortest:
+            T = V_TMP[X]
+            groups = [(0, 1, 2)] + [(2 * k + 1, 2 * k + 2) for k in range(1, 7)] + [(15,)]
+            for gi, grp in enumerate(groups):
+                srcs = ([] if gi == 0 else [T]) + [P + q for q in grp]
+                op = 'v_or3_b32' if len(srcs) == 3 else 'v_or_b32'
+                steps.append((cvt_at[max(grp)] + 3, 3, V(f'{op} v{T}, ' + ', '.join(f'v{r}' for r in srcs), T, srcs)))
+            end = cvt_at[15] + 3
+            steps.append((end + 1, 3, V(f'v_and_b32 v{T}, 0x40004000, v{T}', T, [T])))
+            steps.append((end + 2, 3, V(f'v_cmp_ne_u32 vcc, 0, v{T}', 'vcc', [T])))
         return [x for _, _, x in sorted(steps, key=lambda z: (z[0], z[1]))]
 
     def max_ops(self, X):
@@ -324,6 +355,8 @@ class Gen:
                      rd=[f'v{T + 4}', f'v{T + 5}'], wr=[f'v{T + 4}', f'v{T + 5}']),
                 V(f'v_max_f32 v{T + 6}, v{T + 4}, v{T + 5}', T + 6, [T + 4, T + 5]),
                 V(f'v_cmp_gt_f32 vcc, v{T + 6}, v{mthr}', 'vcc', [T + 6, mthr])]
+        if 'nomax' in PROBE:     # timing probe: a test that never fires
+            out[-1] = V(f'v_cmp_gt_f32 vcc, v{V_NEGINF}, v{mthr}', 'vcc', [V_NEGINF, mthr])
         return out
 
     def softmax_spec(self, X, masked, rescue):
@@ -341,14 +374,20 @@ class Gen:
                 out.append(V(f'v_cmp_lt_i32 vcc, {kofs}, v{V_NVREL}', 'vcc', [V_NVREL]))
                 out.append(Inst(f'v_cndmask_b32 v{S + i}, v{V_NEGINF}, v{S + i}, vcc', 'valu', 4,
                                 rd=[f'v{V_NEGINF}', f'v{S + i}', 'vcc'], wr=[f'v{S + i}']))
-        ex = self.exp_stream(X, mc)
-        mx = self.max_ops(X)
-        # max ops spread over the first 70 % of the exp stream
-        out += merge(ex, [(i, x) for i, x in zip(spread(len(mx), 2, int(len(ex) * 0.7)), mx)])
+        if ORDET:
+            out += probe_filter(self.exp_stream(X, mc, ortest=True), keep_last=True)
+        else:
+            ex = self.exp_stream(X, mc)
+            mx = self.max_ops(X)
+            ex, mx = probe_filter(ex), probe_filter(mx, keep_last=True)
+            # max ops spread over the first 70 % of the exp stream
+            out += merge(ex, [(i, x) for i, x in zip(spread(len(mx), 2, int(len(ex) * 0.7)), mx)])
         resc, ret = self.lab(f'resc{X}'), self.lab(f'ret{X}')
         touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], 32) + ra(A_L[X], 4) + rv(V_ETMP, 16) + rv(P, 16)
+        if MC_BANKS:
+            touched += rv(V_MCB[X], 4)
         out.append(Inst(f's_cbranch_vccnz {resc}\n{ret}:', 'br', 4, rd=['vcc'] + touched, wr=touched))
-        rb = self.rescale_block(X, resc, ret)
+        rb = self.rescale_block_or(X, resc, ret) if ORDET else self.rescale_block(X, resc, ret)
         rb[-2:-2] = self.exp_stream(X, mc)       # recompute P with the new m (before the s_nop 2)
         rescue.append(rb)
         if 'nofill' in PROBE:
@@ -465,6 +504,39 @@ class Gen:
                       wr=[f'v{mc}']))
         b.append(Inst(f'v_cndmask_b32 v{mthr}, v{mthr}, v{T + 1}, vcc', 'valu', rd=[f'v{mthr}', f'v{T + 1}', 'vcc'],
                       wr=[f'v{mthr}']))
+        b += self.scale_acc(X)
+        b.append(raw('s_nop 2'))
+        b.append(raw(f's_branch {ret}'))
+        return b
+
+    def rescale_block_or(self, X, resc, ret):
+        """Out-of-line rescale of the ORDET test: the tile max (max tree) sets m*c = max*c + delta
+        on the lanes where that passes the current m*c (alpha = 2^(mc_old - mc_new)), O_X and the
+        row sums are scaled by alpha, and P is recomputed (appended by the caller)."""
+        T, mc = V_TMP[X], V_MC[X]
+        b = [label(resc), raw('s_nop 4')]
+        b += self.max_ops(X)[:-1]                   # v{T+6} = tile max of the query (raw units)
+        b.append(V(f'v_mul_f32 v{T + 7}, s{S_C}, v{T + 6}', T + 7, [T + 6]))
+        b.append(V(f'v_add_f32 v{T + 7}, {ORDET_DELTA[self.dtype]!r}, v{T + 7}', T + 7, [T + 7]))
+        b.append(V(f'v_cmp_gt_f32 vcc, v{T + 7}, v{mc}', 'vcc', [T + 7, mc]))
+        b.append(V(f'v_sub_f32 v{T}, v{mc}, v{T + 7}', T, [mc, T + 7]))
+        b.append(V(f'v_exp_f32 v{T}, v{T}', T, [T], kind='trans'))
+        b.append(Inst(f'v_cndmask_b32 v{T}, v{V_ONEF}, v{T}, vcc', 'valu', rd=[f'v{V_ONEF}', f'v{T}', 'vcc'],
+                      wr=[f'v{T}']))
+        b.append(Inst(f'v_cndmask_b32 v{mc}, v{mc}, v{T + 7}, vcc', 'valu', rd=[f'v{mc}', f'v{T + 7}', 'vcc'],
+                      wr=[f'v{mc}']))
+        b += self.scale_acc(X)
+        b.append(raw('s_nop 2'))
+        b.append(raw(f's_branch {ret}'))
+        return b
+
+    def scale_acc(self, X):
+        """Rescale tail: m*c copies (MC_BANKS), O_X and the row sums times alpha (v{T})."""
+        T, mc = V_TMP[X], V_MC[X]
+        O, L = A_O[X], A_L[X]
+        b = []
+        if MC_BANKS:
+            b += [V(f'v_mov_b32 v{c}, v{mc}', c, [mc]) for c in range(V_MCB[X], V_MCB[X] + 4)]
         for r in range(32):
             t = T + 2 + (r % 4)
             b.append(Inst(f'v_accvgpr_read_b32 v{t}, a{O + r}', 'accr', rd=[f'a{O + r}'], wr=[f'v{t}']))
@@ -476,8 +548,6 @@ class Gen:
             b.append(Inst(f'v_accvgpr_read_b32 v{t}, a{L + r}', 'accr', rd=[f'a{L + r}'], wr=[f'v{t}']))
             b.append(V(f'v_mul_f32 v{t}, v{t}, v{T + 1}', t, [t, T + 1]))
             b.append(Inst(f'v_accvgpr_write_b32 a{L + r}, v{t}', 'accw', rd=[f'v{t}'], wr=[f'a{L + r}']))
-        b.append(raw('s_nop 2'))
-        b.append(raw(f's_branch {ret}'))
         return b
 
     # ------------------------------------------------------------------ epilogue of a block
@@ -561,6 +631,22 @@ class Gen:
 
 def mark():
     return Inst('', 'mark', 0)
+
+
+def probe_filter(xs, keep_last=False):
+    """Timing probes (--probe): drop or cheapen one instruction class of the softmax stream.
+    keep_last keeps the final instruction (the rescale test) so control flow stays intact."""
+    drop = {'noexp': 'v_exp', 'nofma': 'v_fma', 'nocvt': 'v_cvt', 'nomax': 'v_max'}
+    tail = xs[-1:] if keep_last else []
+    body = xs[:-1] if keep_last else list(xs)
+    for k, pre in drop.items():
+        if k in PROBE:
+            body = [x for x in body if not x.txt.startswith(pre)]
+    if 'expmov' in PROBE:
+        for x in body:
+            if x.txt.startswith('v_exp_f32'):
+                x.txt, x.kind, x.cost = x.txt.replace('v_exp_f32', 'v_mov_b32'), 'valu', 4
+    return body + tail
 
 
 def spread(n, lo, hi):
@@ -1013,6 +1099,8 @@ def prologue(g):
           for r in range(32)]
     p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
     p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in (V_MTHR['A'], V_MTHR['B'], V_MC['A'], V_MC['B'])]
+    if MC_BANKS:
+        p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in range(V_MCB['A'], V_MCB['B'] + 4)]
     p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
     p += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier')]
@@ -1206,6 +1294,9 @@ def main():
     ap.add_argument('--smpipe', type=int, default=None)
     ap.add_argument('--dmap2', type=int, default=None)
     ap.add_argument('--spec', type=int, default=None)
+    ap.add_argument('--ordet', type=int, default=None)
+    ap.add_argument('--lag', default=None, help='EXP_LAG,CVT_LAG')
+    ap.add_argument('--mcbanks', type=int, default=None)
     args = ap.parse_args()
     global DUMP
     if args.dump:
@@ -1224,6 +1315,15 @@ def main():
         SPEC = bool(args.spec)
     if args.dmap2 is not None:
         DMA_P2 = bool(args.dmap2)
+    global ORDET, EXP_LAG, CVT_LAG, MC_BANKS, NVGPR
+    if args.ordet is not None:
+        ORDET = bool(args.ordet)
+    if args.lag:
+        EXP_LAG, CVT_LAG = (int(x) for x in args.lag.split(','))
+    if args.mcbanks is not None:
+        MC_BANKS = bool(args.mcbanks)
+    if MC_BANKS:
+        NVGPR = max(NVGPR, V_MCB['B'] + 4)
     g = Gen(args.dtype)
     blocks, n = build(g)
     txt = emit(g, blocks)

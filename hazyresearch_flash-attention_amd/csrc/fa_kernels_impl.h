@@ -36,8 +36,8 @@ static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipSt
 // per CU) spread the same rows evenly. B4 H12 S2048 D64 (384 workgroups): 793 vs 728 TF/s; C5
 // (256 = one per CU) and C2 (192) keep 8 (808 vs 842, 424 vs 431). With dropout the kernel
 // needs ~168 registers: 8-wave workgroups then fit one per CU (two waves per SIMD), 4-wave
-// ones three per CU, and C3's forward runs 457 vs 369 TF/s. FA_FWD_NW=1 (split-K)|2|4|8 overrides
-// the choice for tuning.
+// ones three per CU, and C3's forward runs 457 vs 369 TF/s. The choice is made here only (no
+// run-time override): 1 = split-K (below), 4 or 8 waves.
 //
 // Split-K (code 1, KSPLIT kernels): when the 8-wave grid has at most one workgroup per CU, each
 // workgroup's latency is the whole kernel, so the two halves of a workgroup take the same 128
@@ -51,11 +51,6 @@ static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipSt
 #endif
 template <int D, bool CAUSAL, bool DROPOUT>
 static int pick_fwd_waves(const FaFwdArgs &a) {
-    static const int forced = [] {
-        const char *e = getenv("FA_FWD_NW");
-        return e ? atoi(e) : 0;
-    }();
-    if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
     if (DROPOUT && D <= 64) return 4;
     const int64_t nwg8 = (int64_t)((a.max_seqlen_q + 255) / 256) * a.nheads * a.batch;
     const int cus = device_cus();
@@ -71,9 +66,8 @@ static hipError_t launch_fwd_t(const FaFwdArgs &a, const FaBlockMask &bm, hipStr
         case 1:
             if constexpr (!CAUSAL && !DROPOUT && D <= 64) return launch_fwd_nw<D, T, false, false, 8, false, true>(a, bm, stream);
             return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
-        case 8: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
         case 4: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 4>(a, bm, stream);
-        default: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 2>(a, bm, stream);
+        default: return launch_fwd_nw<D, T, CAUSAL, DROPOUT, 8>(a, bm, stream);
     }
 }
 

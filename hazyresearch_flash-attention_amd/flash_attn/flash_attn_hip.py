@@ -7,8 +7,11 @@ returning ``softmax_d``. Both accept one extra keyword, ``rng_state=(seed, offse
 the autograd layer can replay a forward's dropout mask without saving the whole RNG state
 (a third element, a device word, carries the offset advance of a captured hipGraph replay).
 
-The library is loaded with ctypes (plain C ABI, include/fa_hip.h). There is no CPU fallback:
-if the shared object is missing every call raises.
+Dense `fwd` / `bwd` calls go through the compiled module `_fa_C` (csrc/fa_torch.cpp: checks,
+allocation and launch in C++, as the reference's pybind11 binding does); block-sparse layouts,
+fused rotary and the helpers load the library with ctypes (plain C ABI, include/fa_hip.h). Both
+drive the same libfa_hip.so. There is no CPU fallback: if the shared object is missing every
+call raises.
 """
 import contextlib
 import ctypes
@@ -20,6 +23,14 @@ import threading
 import torch
 
 _LIB_PATH = os.environ.get("FA_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfa_hip.so"))
+
+# compiled fwd/bwd binding (links the in-tree libfa_hip.so; not used when FA_HIP_LIB points elsewhere)
+_C = None
+if "FA_HIP_LIB" not in os.environ:
+    try:
+        from . import _fa_C as _C
+    except ImportError:
+        _C = None
 
 FA_DTYPE_FP16 = 0
 FA_DTYPE_BF16 = 1
@@ -349,6 +360,13 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
     `rotary` (optional (cos, sin) tables, (>= max_seqlen_q, >= D) in q's dtype) rotates q inside
     the kernel at its load (fused rotary, rotary.py:31-41); k must come rotated already.
     `impl` (FA_IMPL_AUTO / FA_IMPL_HIP) picks the kernel family (include/fa_hip.h)."""
+    if _C is not None and layout is None and rotary is None and q.is_cuda:
+        if p_dropout > 0.0:
+            seed, offset, offset_dev = _unpack_rng(rng_state if rng_state is not None else reserve_rng(q.device, gen))
+        else:
+            seed, offset, offset_dev = 0, 0, None
+        return _C.fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropout, softmax_scale,
+                      zero_tensors, is_causal, return_softmax, seed, offset, offset_dev or 0, impl)
     qdt = q.dtype
     dt = _dtype_code(qdt)
     _check(k.dtype == qdt and v.dtype == qdt, "q, k, v must have the same dtype")
@@ -437,6 +455,13 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
         p_dropout, softmax_scale, zero_tensors, is_causal, gen, rng_state=None, layout=None):
     """Backward pass with the signature flash_attn_interface.py:31-33 expects. Writes dq, dk, dv
     in place (strided views allowed) and returns softmax_d = rowsum(dout * out), (B, H, lse_stride)."""
+    if _C is not None and layout is None and q.is_cuda:
+        if p_dropout > 0.0:
+            seed, offset, offset_dev = _unpack_rng(rng_state if rng_state is not None else reserve_rng(q.device, gen))
+        else:
+            seed, offset, offset_dev = 0, 0, None
+        return _C.bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
+                      max_seqlen_k, p_dropout, softmax_scale, zero_tensors, is_causal, seed, offset, offset_dev or 0)
     dt = _dtype_code(q.dtype)
     for t, n in ((dout, "dout"), (k, "k"), (v, "v"), (out, "out"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
         _check(t.dtype == q.dtype, f"{n} must have the dtype of q")

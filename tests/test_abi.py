@@ -289,3 +289,20 @@ def test_python_checks_raise_runtime_error_on_cpu_tensors():
     cu = torch.tensor([0, 16], dtype=torch.int32)
     with pytest.raises(RuntimeError):
         fi.flash_attn_unpadded_func(q, q, q, cu, cu, 16, 16, 0.0)
+
+
+def test_compiled_binding_loads_and_checks():
+    """flash_attn._fa_C (csrc/fa_torch.cpp) is built next to libfa_hip.so, exposes fwd/bwd with the
+    binding's argument lists and raises the binding's RuntimeErrors before any GPU call."""
+    import torch
+    from flash_attn import flash_attn_hip as hip
+    assert hip._C is not None, "flash_attn/_fa_C.so missing: run hazyresearch_flash-attention_amd/build.py"
+    assert hip._C.version() == hip.lib().fa_version().decode()
+    q = torch.zeros(16, 2, 64, dtype=torch.bfloat16)
+    cu = torch.tensor([0, 16], dtype=torch.int32)
+    with pytest.raises(RuntimeError, match="all tensors must be on the GPU"):
+        hip._C.fwd(q, q, q, cu, cu, 16, 16, 0.0, 0.125, False, False, False, 0, 0, 0, 0)
+    with pytest.raises(RuntimeError, match="FlashAttention only supports fp16 and bf16"):
+        hip._C.fwd(q.float(), q, q, cu, cu, 16, 16, 0.0, 0.125, False, False, False, 0, 0, 0, 0)
+    with pytest.raises(RuntimeError, match="dout must be on the GPU"):
+        hip._C.bwd(q, q, q, q, q, torch.zeros(1, 2, 16), q, q, q, cu, cu, 16, 16, 0.0, 0.125, False, False, 0, 0, 0)

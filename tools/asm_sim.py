@@ -360,7 +360,7 @@ class Sim:
                 res = {'lt': p < q, 'gt': p > q, 'eq': p == q}[kind[:-4]]
             else:
                 p, q = self.vread(w, x), self.vread(w, y)
-                res = {'gt': p > q, 'eq': p == q, 'lt': p < q}[kind[:-4]]
+                res = {'gt': p > q, 'eq': p == q, 'lt': p < q, 'ne': p != q}[kind[:-4]]
             w.vcc = np.asarray(res, dtype=bool)
             return
         if op == 'v_cndmask_b32':
@@ -400,6 +400,8 @@ class Sim:
                 r = src[0] & src[1]
             elif op == 'v_or_b32':
                 r = src[0] | src[1]
+            elif op == 'v_or3_b32':
+                r = src[0] | src[1] | src[2]
             elif op == 'v_xor_b32':
                 r = src[0] ^ src[1]
             elif op == 'v_bfe_u32':

@@ -52,5 +52,5 @@ if a.time:
     ms = s.elapsed_time(e) / a.iters
     fl = 4.0 * a.B * a.H * a.S * Sk * a.D / (2 if a.causal else 1) * (3.5 if a.bwd else 1.0)
     print(f"B={a.B} H={a.H} S={a.S} Sk={Sk} D={a.D} causal={a.causal} p={a.p} bwd={a.bwd} "
-          f"NW={os.environ.get('FA_FWD_NW', 'auto')}: {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOPS")
+          f"{ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOPS")
 print("done")
