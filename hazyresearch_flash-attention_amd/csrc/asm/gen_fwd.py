@@ -52,11 +52,11 @@ TILE = BN * D * 2      # bytes per tile image
 KREG = 0
 VREG = R * TILE
 LDS_BYTES = 2 * R * TILE
-VREADS_P1 = False      # V^T fragment reads of tile j in phase 1 (one phase ahead of PV_A(j))
+VREADS_P1 = True       # V^T fragment reads of tile j in phase 1 (one phase ahead of PV_A(j))
 SM_PIPE = False        # software-pipelined fma -> exp -> cvt order inside the softmax
 DMA_P2 = False         # all four DMA pieces of a tile in phase 2 (K's with V's)
 SPEC = True            # exps against the current max; rescale test branches at the phase end
-ORDET = False          # rescale test = top exponent bit of the packed P (any P >= 2) by an OR tree;
+ORDET = True           # rescale test = top exponent bit of the packed P (any P >= 2) by an OR tree;
 #                        the max tree moves into the out-of-line rescale block
 ORDET_DELTA = {'bf16': 8.0, 'f16': 2.0}   # a rescale sets m = tile max * c + delta (P <= 2^-delta)
 EXP_LAG = 4            # exp_stream: fma(i) -> exp(i) distance (instructions)

@@ -235,6 +235,19 @@ def _fwd_call():
 _tls = threading.local()
 
 
+@contextlib.contextmanager
+def force_impl(impl):
+    """Within the block, forward calls of this thread that leave `impl` at FA_IMPL_AUTO use `impl`
+    instead (e.g. FA_IMPL_HIP: the HIP kernels for every shape, so that a result can be compared
+    bit for bit with a path the assembly forward does not serve, such as fused rotary)."""
+    prev = getattr(_tls, "impl", FA_IMPL_AUTO)
+    _tls.impl = impl
+    try:
+        yield
+    finally:
+        _tls.impl = prev
+
+
 def _on_device(dev):
     # the reference runs under a CUDAGuard for q's device (fmha_api.cpp:184)
     if dev.index is None or dev.index == torch.cuda.current_device():
@@ -360,6 +373,8 @@ def fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, p_dropo
     `rotary` (optional (cos, sin) tables, (>= max_seqlen_q, >= D) in q's dtype) rotates q inside
     the kernel at its load (fused rotary, rotary.py:31-41); k must come rotated already.
     `impl` (FA_IMPL_AUTO / FA_IMPL_HIP) picks the kernel family (include/fa_hip.h)."""
+    if impl == FA_IMPL_AUTO:
+        impl = getattr(_tls, "impl", FA_IMPL_AUTO)
     if _C is not None and layout is None and rotary is None and q.is_cuda:
         if p_dropout > 0.0:
             seed, offset, offset_dev = _unpack_rng(rng_state if rng_state is not None else reserve_rng(q.device, gen))

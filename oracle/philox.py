@@ -71,3 +71,39 @@ def dropout_keep_mask(seed, offset, p_dropout, batch, nheads, seqlen_q, seqlen_k
         for h in range(nheads):
             m[b, h] = rnd16(seed, offset, b * nheads + h, rows, cols) <= thr
     return m
+
+
+def philox4x32_torch(c0, c1, c2, c3, k0, k1, rounds=7):
+    """philox4x32 on int64 torch tensors holding uint32 values (any device): the same rounds as
+    philox4x32 above; products wrap modulo 2^64 and the & masks recover the 32-bit halves."""
+    m = 0xFFFFFFFF
+    for _ in range(rounds):
+        p0 = c0 * int(M0)
+        p1 = c2 * int(M1)
+        c0, c1, c2, c3 = ((p1 >> 32) & m) ^ c1 ^ k0, p1 & m, ((p0 >> 32) & m) ^ c3 ^ k1, p0 & m
+        k0 = (k0 + W0) & m
+        k1 = (k1 + W1) & m
+    return c0, c1, c2, c3
+
+
+def dropout_keep_mask_torch(seed, offset, p_dropout, batch, nheads, seqlen_q, seqlen_k, device):
+    """dropout_keep_mask evaluated with torch on `device` (the exact-grid GPU tests need the
+    8x12x2048x2048 mask in seconds): one Philox call per (b*H + h, g, col) covers the 8 rows of
+    group g, word slot >> 1, half slot & 1, exactly as rnd16 maps them."""
+    import torch
+    thr = keep_threshold(p_dropout)
+    rows = torch.arange(seqlen_q, device=device)
+    g = ((rows >> 5) << 2) | (((rows >> 4) & 1) << 1) | ((rows >> 2) & 1)
+    slot = (rows & 3) | (((rows >> 3) & 1) << 2)
+    ng = int(g.max().item()) + 1
+    gg = torch.arange(ng, device=device, dtype=torch.int64)[:, None].expand(ng, seqlen_k)
+    cc = torch.arange(seqlen_k, device=device, dtype=torch.int64)[None, :].expand(ng, seqlen_k)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    c3 = torch.full_like(gg, (offset >> 2) & 0xFFFFFFFF)
+    out = torch.empty((batch, nheads, seqlen_q, seqlen_k), dtype=torch.bool, device=device)
+    for bh in range(batch * nheads):
+        w = torch.stack(philox4x32_torch(gg, cc, torch.full_like(gg, bh), c3, k0, k1))   # (4, ng, Sk)
+        word = w[(slot >> 1), g]                                                     # (Sq, Sk)
+        r16 = (word >> (16 * (slot & 1))[:, None]) & 0xFFFF
+        out[bh // nheads, bh % nheads] = r16 <= thr
+    return out

@@ -13,7 +13,8 @@ import pytest
 import torch
 
 from fa_testutil import convert_s_dmask
-from oracle.attention_ref import attention_blocksparse_ref, generate_random_padding_mask, max_err_bound, pad, unpad
+from oracle.attention_ref import (attention_blocksparse_ref, attention_ref, generate_random_padding_mask, max_err_bound,
+                                  pad, unpad)
 from oracle.philox import dropout_keep_mask
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "blocksparse_golden.npz")
@@ -168,8 +169,17 @@ def test_blocksparse_full_layout_matches_dense():
     cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=DEV)
     layout = torch.ones((S + 15) // 16, (S + 255) // 256, dtype=torch.bool, device=DEV)
     o_bs = bsi.flash_blocksparse_attn_func(qkv, cu, layout, 0.0, S)
-    o_d = flash_attn_unpadded_qkvpacked_func(qkv, cu, S, 0.0)
+    # bitwise against the HIP dense kernel (impl=FA_IMPL_HIP); the default dense path for this shape
+    # is the assembly forward, which sums rows in another order: within the 2x rule of the oracle
+    from flash_attn import flash_attn_hip as hip
+    o_d = hip.fwd(qkv[:, 0], qkv[:, 1], qkv[:, 2], cu, cu, S, S, 0.0, D ** -0.5, False, False, False, None,
+                  impl=hip.FA_IMPL_HIP)[0]
     assert torch.equal(o_bs, o_d)
+    o_auto = flash_attn_unpadded_qkvpacked_func(qkv, cu, S, 0.0)
+    q4, k4, v4 = (qkv[:, i].view(B, S, H, D) for i in range(3))
+    ref, _ = attention_ref(q4, k4, v4)
+    pt, _ = attention_ref(q4, k4, v4, upcast=False, reorder_ops=True)
+    assert (o_auto.view(B, S, H, D).float() - ref.float()).abs().max().item() <= max_err_bound(pt, ref)
 
 
 @pytest.mark.gpu

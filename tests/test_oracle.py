@@ -51,6 +51,14 @@ def test_rng_numpy_matches_c():
         assert int(philox.rnd16(seed, offset, bh, [row], [col])[0, 0]) == tiled.rnd16(seed, offset, bh, row, col)
 
 
+@pytest.mark.parametrize("seed,offset,Sq,Sk", [(0x1234567890ABCDEF, 8, 200, 130), (2 ** 63 - 25, 4 * 77777, 97, 257)])
+def test_torch_keep_mask_matches_numpy(seed, offset, Sq, Sk):
+    """The torch restatement used by the exact-grid GPU tests equals the numpy oracle bit for bit."""
+    ref = philox.dropout_keep_mask(seed, offset, 0.1, 2, 3, Sq, Sk)
+    got = philox.dropout_keep_mask_torch(seed, offset, 0.1, 2, 3, Sq, Sk, "cpu").numpy()
+    assert np.array_equal(ref, got)
+
+
 def test_rng_element_map_is_bijective_per_call():
     """Each Philox call feeds 8 distinct rows of one column; all rows of a 32-block are covered."""
     rows = np.arange(64)
