@@ -2,17 +2,18 @@
 //
 // The reference binds its kernels as the pybind11 module `flash_attn_cuda` (fmha_api.cpp:244-247):
 // argument checks, output allocation and the launch all run in C++. This module does the same
-// over the C ABI (include/fa_hip.h) for the two calls on the training path, `fwd` and `bwd`, so
-// the per-call host cost is one pybind11 dispatch, the at::empty allocations and the launch.
-// flash_attn_hip.py routes its dense calls here (block-sparse layouts and fused rotary keep the
-// ctypes path) and keeps the dropout RNG reservation in Python (reserve_rng), passing the
-// reserved (seed, offset, device word) in.
+// over the C ABI (include/fa_hip.h) for the calls on the training path: `fwd` and `bwd`, and the
+// autograd functions of flash_attn_interface / flash_attention (below), so the per-call host cost
+// is one pybind11 dispatch, the at::empty allocations and the launch. flash_attn_hip.py routes its
+// dense calls here (block-sparse layouts keep the ctypes path) and keeps the dropout RNG
+// reservation in Python (reserve_rng), passing the reserved (seed, offset, device word) in.
 //
 // Checks and error messages are the ones flash_attn_hip.py raises (RuntimeError through
 // TORCH_CHECK, as fmha_api.cpp:131-170 does).
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
+#include <torch/csrc/autograd/custom_function.h>
 #include <torch/csrc/utils/pybind.h>
 
 #include <cmath>
@@ -73,7 +74,8 @@ bool bwd_needs_workspace(int64_t head_dim, bool dropout) {
 std::vector<at::Tensor> fwd(at::Tensor q, at::Tensor k, at::Tensor v, const at::Tensor &cu_q, const at::Tensor &cu_k,
                             int64_t max_seqlen_q, int64_t max_seqlen_k, double p_dropout, double softmax_scale,
                             bool zero_tensors, bool is_causal, bool return_softmax, uint64_t seed, uint64_t offset,
-                            int64_t offset_dev, int64_t impl) {
+                            int64_t offset_dev, int64_t impl, const c10::optional<at::Tensor> &rot_cos = c10::nullopt,
+                            const c10::optional<at::Tensor> &rot_sin = c10::nullopt) {
     const auto qdt = q.scalar_type();
     const int dt = dtype_code(qdt);
     TORCH_CHECK(k.scalar_type() == qdt && v.scalar_type() == qdt, "q, k, v must have the same dtype");
@@ -143,6 +145,19 @@ std::vector<at::Tensor> fwd(at::Tensor q, at::Tensor k, at::Tensor v, const at::
     a.is_causal = is_causal ? 1 : 0;
     a.dtype = dt;
     a.impl = (int32_t)impl;
+    if (rot_cos && rot_cos->defined()) {
+        // flash_attn_hip.fwd(rotary=(cos, sin)): q rotated at the kernel's Q load
+        TORCH_CHECK(rot_sin && rot_sin->defined(), "rotary needs both cos and sin tables");
+        const at::Tensor &c = *rot_cos, &sn = *rot_sin;
+        TORCH_CHECK(c.scalar_type() == qdt && sn.scalar_type() == qdt && c.is_cuda() && sn.is_cuda(),
+                    "rotary tables must be on the GPU in q's dtype");
+        TORCH_CHECK(c.dim() == 2 && c.stride(-1) == 1 && c.strides() == sn.strides() && c.sizes() == sn.sizes() &&
+                        c.size(0) >= max_seqlen_q && c.size(1) >= head_dim,
+                    "rotary tables must be (>= max_seqlen_q, >= head_dim) with one row stride");
+        a.rot_cos = c.data_ptr();
+        a.rot_sin = sn.data_ptr();
+        a.rot_stride = c.stride(0);
+    }
     const int rc = fa_fwd(&a, current_stream(dev));
     if (rc != 0) raise_rc(rc, "fa_fwd");
     std::vector<at::Tensor> res{o, lse};
@@ -238,11 +253,249 @@ at::Tensor bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Te
     return softmax_d;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Autograd functions of flash_attn_interface (FlashAttnFunc / FlashAttnKVPackedFunc /
+// FlashAttnQKVPackedFunc, reference flash_attn_interface.py:39-252) and of the fused-rotary
+// FlashAttnRotaryQKVFunc (flash_attention.py), in C++: one pybind11 call per forward, the
+// backward node runs without Python. The Python classes stay for return_attn_probs=True.
+// Dropout: the caller reserves (seed, offset[, device word]) from the torch generator exactly as
+// the Python functions do (flash_attn_hip.reserve_rng) and passes them in; they are saved for the
+// backward (the device word as a tensor, so a captured graph's word outlives the forward).
+// ---------------------------------------------------------------------------------------------
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+
+struct Saved {
+    int64_t max_q, max_k;
+    double p, scale;
+    bool causal;
+    uint64_t seed, offset;
+    at::Tensor od;
+};
+
+void save_cfg(AutogradContext *ctx, int64_t max_q, int64_t max_k, double p, double scale, bool causal, uint64_t seed,
+              uint64_t offset, const c10::optional<at::Tensor> &od) {
+    ctx->saved_data["mq"] = max_q;
+    ctx->saved_data["mk"] = max_k;
+    ctx->saved_data["p"] = p;
+    ctx->saved_data["sc"] = scale;
+    ctx->saved_data["ca"] = causal;
+    ctx->saved_data["se"] = (int64_t)seed;
+    ctx->saved_data["of"] = (int64_t)offset;
+    if (od && od->defined()) ctx->saved_data["od"] = *od;
+}
+
+Saved load_cfg(AutogradContext *ctx) {
+    Saved s;
+    s.max_q = ctx->saved_data["mq"].toInt();
+    s.max_k = ctx->saved_data["mk"].toInt();
+    s.p = ctx->saved_data["p"].toDouble();
+    s.scale = ctx->saved_data["sc"].toDouble();
+    s.causal = ctx->saved_data["ca"].toBool();
+    s.seed = (uint64_t)ctx->saved_data["se"].toInt();
+    s.offset = (uint64_t)ctx->saved_data["of"].toInt();
+    auto it = ctx->saved_data.find("od");
+    if (it != ctx->saved_data.end() && it->second.isTensor()) s.od = it->second.toTensor();
+    return s;
+}
+
+int64_t od_ptr(const c10::optional<at::Tensor> &od) {
+    return od && od->defined() ? reinterpret_cast<int64_t>(od->data_ptr()) : 0;
+}
+
+int64_t od_ptr(const at::Tensor &od) { return od.defined() ? reinterpret_cast<int64_t>(od.data_ptr()) : 0; }
+
+// true when autograd would record a node (grad mode on and some input requires grad); otherwise
+// the entry points call the forward directly, which is what apply would run
+bool needs_grad(std::initializer_list<const at::Tensor *> ts) {
+    if (!at::GradMode::is_enabled()) return false;
+    for (const at::Tensor *t : ts)
+        if (t->requires_grad()) return true;
+    return false;
+}
+
+struct FlashAttnFn : public torch::autograd::Function<FlashAttnFn> {
+    static variable_list forward(AutogradContext *ctx, const at::Tensor &q, const at::Tensor &k, const at::Tensor &v,
+                                 const at::Tensor &cu_q, const at::Tensor &cu_k, int64_t max_q, int64_t max_k, double p,
+                                 double scale, bool causal, uint64_t seed, uint64_t offset,
+                                 const c10::optional<at::Tensor> &od, int64_t impl) {
+        auto r = fwd(q, k, v, cu_q, cu_k, max_q, max_k, p, scale, false, causal, false, seed, offset, od_ptr(od), impl);
+        ctx->save_for_backward({q, k, v, r[0], r[1], cu_q, cu_k});
+        save_cfg(ctx, max_q, max_k, p, scale, causal, seed, offset, od);
+        return {r[0]};
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list g) {
+        auto t = ctx->get_saved_variables();
+        Saved s = load_cfg(ctx);
+        at::Tensor dq = at::empty_like(t[0]), dk = at::empty_like(t[1]), dv = at::empty_like(t[2]);
+        bwd(g[0], t[0], t[1], t[2], t[3], t[4], dq, dk, dv, t[5], t[6], s.max_q, s.max_k, s.p, s.scale, false,
+            s.causal, s.seed, s.offset, od_ptr(s.od));
+        at::Tensor n;
+        return {dq, dk, dv, n, n, n, n, n, n, n, n, n, n, n};
+    }
+};
+
+struct FlashAttnKVPackedFn : public torch::autograd::Function<FlashAttnKVPackedFn> {
+    static variable_list forward(AutogradContext *ctx, const at::Tensor &q, const at::Tensor &kv,
+                                 const at::Tensor &cu_q, const at::Tensor &cu_k, int64_t max_q, int64_t max_k, double p,
+                                 double scale, bool causal, uint64_t seed, uint64_t offset,
+                                 const c10::optional<at::Tensor> &od, int64_t impl) {
+        TORCH_CHECK(kv.dim() == 4 && kv.size(1) == 2, "kv must be (total_k, 2, nheads, headdim)");
+        auto r = fwd(q, kv.select(1, 0), kv.select(1, 1), cu_q, cu_k, max_q, max_k, p, scale, false, causal, false,
+                     seed, offset, od_ptr(od), impl);
+        ctx->save_for_backward({q, kv, r[0], r[1], cu_q, cu_k});
+        save_cfg(ctx, max_q, max_k, p, scale, causal, seed, offset, od);
+        return {r[0]};
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list g) {
+        auto t = ctx->get_saved_variables();
+        Saved s = load_cfg(ctx);
+        at::Tensor dq = at::empty_like(t[0]), dkv = at::empty_like(t[1]);
+        bwd(g[0], t[0], t[1].select(1, 0), t[1].select(1, 1), t[2], t[3], dq, dkv.select(1, 0), dkv.select(1, 1),
+            t[4], t[5], s.max_q, s.max_k, s.p, s.scale, false, s.causal, s.seed, s.offset, od_ptr(s.od));
+        at::Tensor n;
+        return {dq, dkv, n, n, n, n, n, n, n, n, n, n, n};
+    }
+};
+
+struct FlashAttnQKVPackedFn : public torch::autograd::Function<FlashAttnQKVPackedFn> {
+    static variable_list forward(AutogradContext *ctx, const at::Tensor &qkv, const at::Tensor &cu, int64_t max_s,
+                                 double p, double scale, bool causal, uint64_t seed, uint64_t offset,
+                                 const c10::optional<at::Tensor> &od, int64_t impl) {
+        TORCH_CHECK(qkv.dim() == 4 && qkv.size(1) == 3, "qkv must be (total, 3, nheads, headdim)");
+        auto r = fwd(qkv.select(1, 0), qkv.select(1, 1), qkv.select(1, 2), cu, cu, max_s, max_s, p, scale, false,
+                     causal, false, seed, offset, od_ptr(od), impl);
+        ctx->save_for_backward({qkv, r[0], r[1], cu});
+        save_cfg(ctx, max_s, max_s, p, scale, causal, seed, offset, od);
+        return {r[0]};
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list g) {
+        auto t = ctx->get_saved_variables();
+        Saved s = load_cfg(ctx);
+        at::Tensor dqkv = at::empty_like(t[0]);
+        bwd(g[0], t[0].select(1, 0), t[0].select(1, 1), t[0].select(1, 2), t[1], t[2], dqkv.select(1, 0),
+            dqkv.select(1, 1), dqkv.select(1, 2), t[3], t[3], s.max_q, s.max_k, s.p, s.scale, false, s.causal, s.seed,
+            s.offset, od_ptr(s.od));
+        at::Tensor n;
+        return {dqkv, n, n, n, n, n, n, n, n, n};
+    }
+};
+
+// fa_rotary over (B, S, NSLOT, H, D) views given by element strides (flash_attn_hip.rotary)
+void rotary_call(const at::Tensor &x, const at::Tensor &y, const at::Tensor &cos, const at::Tensor &sin,
+                 std::array<int64_t, 5> shape, std::array<int64_t, 4> xs, std::array<int64_t, 4> ys, int nrot,
+                 bool inverse) {
+    TORCH_CHECK(cos.stride(0) == sin.stride(0), "cos and sin tables must share a row stride");
+    FaRotaryArgs r{};
+    r.x = x.data_ptr();
+    r.y = y.data_ptr();
+    r.cos = cos.data_ptr();
+    r.sin = sin.data_ptr();
+    for (int i = 0; i < 4; ++i) {
+        r.x_strides[i] = xs[i];
+        r.y_strides[i] = ys[i];
+    }
+    r.table_stride = cos.stride(0);
+    r.batch = (int32_t)shape[0];
+    r.seqlen = (int32_t)shape[1];
+    r.nslot = (int32_t)shape[2];
+    r.nheads = (int32_t)shape[3];
+    r.head_dim = (int32_t)shape[4];
+    r.nrot = nrot;
+    r.inverse = inverse ? 1 : 0;
+    r.dtype = dtype_code(x.scalar_type());
+    const int rc = fa_rotary(&r, current_stream(x.device()));
+    if (rc != 0) raise_rc(rc, "fa_rotary");
+}
+
+// FlashAttnRotaryQKVFunc (flash_attention.py): padded contiguous qkv (B, S, 3, H, D); k rotated by
+// one fa_rotary pass, q rotated inside the forward at its load; backward rotates q once more, runs
+// the attention backward on (q_rot, k_rot, v) and rotates dq, dk back in place.
+struct FlashAttnRotaryQKVFn : public torch::autograd::Function<FlashAttnRotaryQKVFn> {
+    static variable_list forward(AutogradContext *ctx, const at::Tensor &qkv, const at::Tensor &cos_in,
+                                 const at::Tensor &sin_in, const at::Tensor &cu, double p, double scale, bool causal,
+                                 uint64_t seed, uint64_t offset, const c10::optional<at::Tensor> &od) {
+        TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.is_contiguous(), "qkv must be contiguous (B, S, 3, H, D)");
+        const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
+        c10::DeviceGuard guard(qkv.device());
+        at::Tensor cos = cos_in.slice(0, 0, S).contiguous(), sin = sin_in.slice(0, 0, S).contiguous();
+        at::Tensor k_rot = at::empty({B, S, H, D}, qkv.options());
+        rotary_call(qkv.select(2, 1), k_rot, cos, sin, {B, S, 1, H, D}, {S * 3 * H * D, 3 * H * D, 0, D},
+                    {S * H * D, H * D, 0, D}, 1, false);
+        at::Tensor flat = qkv.view({B * S, 3, H, D});
+        auto r = fwd(flat.select(1, 0), k_rot.view({B * S, H, D}), flat.select(1, 2), cu, cu, S, S, p, scale, false,
+                     causal, false, seed, offset, od_ptr(od), FA_IMPL_AUTO, cos, sin);
+        ctx->save_for_backward({qkv, k_rot, r[0], r[1], cos, sin, cu});
+        save_cfg(ctx, S, S, p, scale, causal, seed, offset, od);
+        return {r[0].view({B, S, H, D})};
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list g) {
+        auto t = ctx->get_saved_variables();
+        Saved s = load_cfg(ctx);
+        const at::Tensor &qkv = t[0], &k_rot = t[1], &out = t[2], &lse = t[3], &cos = t[4], &sin = t[5], &cu = t[6];
+        const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
+        c10::DeviceGuard guard(qkv.device());
+        at::Tensor q_rot = at::empty({B, S, H, D}, qkv.options());
+        rotary_call(qkv.select(2, 0), q_rot, cos, sin, {B, S, 1, H, D}, {S * 3 * H * D, 3 * H * D, 0, D},
+                    {S * H * D, H * D, 0, D}, 1, false);
+        at::Tensor dqkv = at::empty_like(qkv);
+        at::Tensor d = dqkv.view({B * S, 3, H, D});
+        bwd(g[0].reshape({B * S, H, D}), q_rot.view({B * S, H, D}), k_rot.view({B * S, H, D}),
+            qkv.view({B * S, 3, H, D}).select(1, 2), out, lse, d.select(1, 0), d.select(1, 1), d.select(1, 2), cu, cu,
+            S, S, s.p, s.scale, false, s.causal, s.seed, s.offset, od_ptr(s.od));
+        const std::array<int64_t, 4> st3{S * 3 * H * D, 3 * H * D, H * D, D};
+        rotary_call(dqkv, dqkv, cos, sin, {B, S, 3, H, D}, st3, st3, 2, true);   // dq, dk back; dv as is
+        at::Tensor n;
+        return {dqkv, n, n, n, n, n, n, n, n, n};
+    }
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_fa_C, m) {
     m.doc() = "compiled binding of libfa_hip.so (fwd / bwd over include/fa_hip.h)";
-    m.def("fwd", &fwd);
+    m.def("fwd", &fwd, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("cu_q"),
+          pybind11::arg("cu_k"), pybind11::arg("max_seqlen_q"), pybind11::arg("max_seqlen_k"), pybind11::arg("p_dropout"),
+          pybind11::arg("softmax_scale"), pybind11::arg("zero_tensors"), pybind11::arg("is_causal"),
+          pybind11::arg("return_softmax"), pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("offset_dev"),
+          pybind11::arg("impl"), pybind11::arg("rot_cos") = pybind11::none(), pybind11::arg("rot_sin") = pybind11::none());
     m.def("bwd", &bwd);
+    m.def("flash_attn_unpadded_func",
+          [](const at::Tensor &q, const at::Tensor &k, const at::Tensor &v, const at::Tensor &cu_q, const at::Tensor &cu_k,
+             int64_t max_q, int64_t max_k, double p, c10::optional<double> scale_opt, bool causal, uint64_t seed,
+             uint64_t offset, const c10::optional<at::Tensor> &od, int64_t impl) {
+              const double scale = scale_opt ? *scale_opt : 1.0 / std::sqrt((double)q.size(-1));
+              if (!needs_grad({&q, &k, &v}))   // no graph to record: the forward alone, same result
+                  return fwd(q, k, v, cu_q, cu_k, max_q, max_k, p, scale, false, causal, false, seed, offset, od_ptr(od),
+                             impl)[0];
+              return FlashAttnFn::apply(q, k, v, cu_q, cu_k, max_q, max_k, p, scale, causal, seed, offset, od, impl)[0];
+          });
+    m.def("flash_attn_unpadded_kvpacked_func",
+          [](const at::Tensor &q, const at::Tensor &kv, const at::Tensor &cu_q, const at::Tensor &cu_k, int64_t max_q,
+             int64_t max_k, double p, c10::optional<double> scale_opt, bool causal, uint64_t seed, uint64_t offset,
+             const c10::optional<at::Tensor> &od, int64_t impl) {
+              const double scale = scale_opt ? *scale_opt : 1.0 / std::sqrt((double)q.size(-1));
+              TORCH_CHECK(kv.dim() == 4 && kv.size(1) == 2, "kv must be (total_k, 2, nheads, headdim)");
+              if (!needs_grad({&q, &kv}))
+                  return fwd(q, kv.select(1, 0), kv.select(1, 1), cu_q, cu_k, max_q, max_k, p, scale, false, causal,
+                             false, seed, offset, od_ptr(od), impl)[0];
+              return FlashAttnKVPackedFn::apply(q, kv, cu_q, cu_k, max_q, max_k, p, scale, causal, seed, offset, od,
+                                                impl)[0];
+          });
+    m.def("flash_attn_unpadded_qkvpacked_func",
+          [](const at::Tensor &qkv, const at::Tensor &cu, int64_t max_s, double p, c10::optional<double> scale_opt,
+             bool causal, uint64_t seed, uint64_t offset, const c10::optional<at::Tensor> &od, int64_t impl) {
+              const double scale = scale_opt ? *scale_opt : 1.0 / std::sqrt((double)qkv.size(-1));
+              TORCH_CHECK(qkv.dim() == 4 && qkv.size(1) == 3, "qkv must be (total, 3, nheads, headdim)");
+              if (!needs_grad({&qkv}))
+                  return fwd(qkv.select(1, 0), qkv.select(1, 1), qkv.select(1, 2), cu, cu, max_s, max_s, p, scale,
+                             false, causal, false, seed, offset, od_ptr(od), impl)[0];
+              return FlashAttnQKVPackedFn::apply(qkv, cu, max_s, p, scale, causal, seed, offset, od, impl)[0];
+          });
+    m.def("flash_attn_rotary_qkv_func",
+          [](const at::Tensor &qkv, const at::Tensor &cos, const at::Tensor &sin, const at::Tensor &cu, double p,
+             double scale, bool causal, uint64_t seed, uint64_t offset, const c10::optional<at::Tensor> &od) {
+              return FlashAttnRotaryQKVFn::apply(qkv, cos, sin, cu, p, scale, causal, seed, offset, od)[0];
+          });
     m.def("version", [] { return std::string(fa_version()); });
 }

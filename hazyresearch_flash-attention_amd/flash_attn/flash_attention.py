@@ -53,7 +53,26 @@ class FlashAttention(nn.Module):
         return out.reshape(batch, seqlen, nheads, -1), None
 
 
-class FlashAttnRotaryQKVFunc(torch.autograd.Function):
+class FlashAttnRotaryQKVFunc:
+    """Entry point of the fused-rotary attention: `apply(qkv, cos, sin, dropout_p, softmax_scale,
+    causal)` runs the compiled autograd function (csrc/fa_torch.cpp FlashAttnRotaryQKVFn, one
+    pybind11 call) when the binding is built and qkv is on the GPU, else the Python one below
+    (same kernels, same results)."""
+
+    @staticmethod
+    def apply(qkv, cos, sin, dropout_p, softmax_scale, causal):
+        from flash_attn import flash_attn_hip as hip
+        C = hip._C
+        if C is None or not qkv.is_cuda:
+            return _FlashAttnRotaryQKVFuncPy.apply(qkv, cos, sin, dropout_p, softmax_scale, causal)
+        B, S, _, H, D = qkv.shape
+        seed, offset, od = hip._rng_args(dropout_p, qkv.device)
+        return C.flash_attn_rotary_qkv_func(qkv, cos, sin, _uniform_cu_seqlens(B, S, qkv.device), dropout_p,
+                                            D ** -0.5 if softmax_scale is None else softmax_scale, causal,
+                                            seed, offset, od)
+
+
+class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
     """Attention over a padded, contiguous qkv (B, S, 3, H, D) with rotary embeddings fused into
     the forward (README.md:56 "Fuse rotary embedding"; rotation = rotary.py:31-41):
     * forward: k is rotated by one fa_rotary pass into a (B, S, H, D) buffer (the backward needs it

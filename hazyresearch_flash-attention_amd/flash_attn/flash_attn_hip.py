@@ -317,6 +317,18 @@ def reserve_rng(device, gen=None, increment=None):
     return int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset), offset_dev
 
 
+def _rng_args(p_dropout, device):
+    """(seed, offset, device word or None) for one dropout call (reserve_rng), zeros without dropout:
+    the arguments the compiled autograd functions (_fa_C) take and save for their backward."""
+    if p_dropout > 0.0:
+        return reserve_rng(device)
+    return 0, 0, None
+
+
+def _impl():
+    return getattr(_tls, "impl", FA_IMPL_AUTO)
+
+
 def _unpack_rng(rng_state):
     seed, offset = rng_state[0], rng_state[1]
     dev_word = rng_state[2] if len(rng_state) > 2 else None

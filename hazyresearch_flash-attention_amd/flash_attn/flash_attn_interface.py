@@ -9,7 +9,10 @@ Same public names, argument order, defaults and return values as the reference m
   that pair in ctx, instead of snapshotting the whole RNG state (:44, :60-63, :70-71);
 * `S_dmask` (return_attn_probs=True) is row-major (B, H, round16(max_q), round16(max_k)),
   holds softmax probabilities already normalised, negated where dropout dropped the entry,
-  and 0 outside the valid (and causal) region.
+  and 0 outside the valid (and causal) region;
+* the three autograd functions run in C++ (csrc/fa_torch.cpp, module _fa_C) when the compiled
+  binding is built and the inputs are on the GPU: one pybind11 call per forward, a C++ backward
+  node. The Python classes below are the same computation and serve return_attn_probs=True.
 """
 import torch
 
@@ -38,6 +41,9 @@ def _flash_attn_backward(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens
         dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
         max_seqlen_q, max_seqlen_k, dropout_p, softmax_scale, False, causal, None, rng_state=rng_state)
     return dq, dk, dv, softmax_d
+
+
+_NO_RNG = (0, 0, None)
 
 
 def _reserve(dropout_p, device):
@@ -142,6 +148,11 @@ def flash_attn_unpadded_qkvpacked_func(qkv, cu_seqlens, max_seqlen, dropout_p, s
     """Attention over packed qkv (total, 3, nheads, headdim); cu_seqlens (batch+1,) int32.
     Returns out (total, nheads, headdim), or (out, softmax_lse, S_dmask) with return_attn_probs.
     softmax_scale defaults to headdim**-0.5. Set dropout_p to 0.0 for evaluation."""
+    C = _hip._C
+    if C is not None and not return_attn_probs and qkv.is_cuda:
+        seed, offset, od = _hip._rng_args(dropout_p, qkv.device) if dropout_p > 0 else _NO_RNG
+        return C.flash_attn_unpadded_qkvpacked_func(qkv, cu_seqlens, max_seqlen, dropout_p, softmax_scale, causal,
+                                                    seed, offset, od, _hip._impl())
     return FlashAttnQKVPackedFunc.apply(qkv, cu_seqlens, max_seqlen, dropout_p, softmax_scale,
                                         causal, return_attn_probs)
 
@@ -150,6 +161,11 @@ def flash_attn_unpadded_kvpacked_func(q, kv, cu_seqlens_q, cu_seqlens_k, max_seq
                                       dropout_p, softmax_scale=None, causal=False,
                                       return_attn_probs=False):
     """Attention with q (total_q, nheads, headdim) and packed kv (total_k, 2, nheads, headdim)."""
+    C = _hip._C
+    if C is not None and not return_attn_probs and q.is_cuda:
+        seed, offset, od = _hip._rng_args(dropout_p, q.device) if dropout_p > 0 else _NO_RNG
+        return C.flash_attn_unpadded_kvpacked_func(q, kv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
+                                                   dropout_p, softmax_scale, causal, seed, offset, od, _hip._impl())
     return FlashAttnKVPackedFunc.apply(q, kv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
                                        dropout_p, softmax_scale, causal, return_attn_probs)
 
@@ -157,6 +173,11 @@ def flash_attn_unpadded_kvpacked_func(q, kv, cu_seqlens_q, cu_seqlens_k, max_seq
 def flash_attn_unpadded_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
                              dropout_p, softmax_scale=None, causal=False, return_attn_probs=False):
     """Attention with separate q (total_q, nheads, headdim), k and v (total_k, nheads, headdim)."""
+    C = _hip._C
+    if C is not None and not return_attn_probs and q.is_cuda:
+        seed, offset, od = _hip._rng_args(dropout_p, q.device) if dropout_p > 0 else _NO_RNG
+        return C.flash_attn_unpadded_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, dropout_p,
+                                          softmax_scale, causal, seed, offset, od, _hip._impl())
     return FlashAttnFunc.apply(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
                                dropout_p, softmax_scale, causal, return_attn_probs)
 
