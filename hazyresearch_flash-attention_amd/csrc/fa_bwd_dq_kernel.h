@@ -32,7 +32,7 @@ struct DqCfg {
 };
 
 template <int D, typename T, bool CAUSAL, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a) {
+__global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a, const int slots) {
     using C = DqCfg<D, NW>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
@@ -43,7 +43,12 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a
     const int nbh = gridDim.y * gridDim.z;
     const int L = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
     int qb, bh_lin;
-    if (CAUSAL) {
+    if (FA_BWD_XCD && CAUSAL) {
+        // heaviest (last) query blocks first within XCD head groups (xcd_grouped)
+        int rank;
+        xcd_grouped(L, nqb, nbh, slots, rank, bh_lin);
+        qb = nqb - 1 - rank;
+    } else if (CAUSAL) {
         qb = nqb - 1 - L / nbh;
         bh_lin = L % nbh;
     } else {

@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_convert_kernel(const FaBwdArgs 
 #define FA_BWD_BOUNDS(C) __launch_bounds__((64 * BwdWaves<C>::value), 2)
 // DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
-__global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaBlockMask bm) {
+__global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaBlockMask bm, const int slots) {
     static_assert(D <= 64, "D = 128 takes fa_bwd_split_kernel");
     using C = BwdCfg<D, BwdWaves<CAUSAL>::value, CAUSAL>;
     using S = Swz<D>;
@@ -143,10 +143,29 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     float *lse_s = (float *)(smem + C::OFF_LSE);
     float *del_s = (float *)(smem + C::OFF_DELTA);
 
-    // causal: key block kb sees queries kb*BKV..end, so block 0 is the heaviest: launch all
-    // heads' block 0 first, then block 1, ... (LPT order)
+    // causal: key block kb sees queries kb*BKV..end, so block 0 is the heaviest. FA_BWD_XCD:
+    // causal in xcd_grouped order (block 0 first within XCD head groups), non-causal head-major
+    // per XCD (xcd_contiguous); else all heads' block 0 first, then block 1, ... (global order)
     int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    if (CAUSAL) {
+    if (FA_BWD_XCD) {
+        const int nkb = gridDim.x, nbh = gridDim.y * gridDim.z;
+        const int L = blockIdx.x + nkb * (blockIdx.y + gridDim.y * blockIdx.z);
+        int bh;
+        if (CAUSAL && DQ) {
+            // dQ by fp32 atomics: a group's key blocks would all add into the same dQ rows at
+            // once (C3: 315 vs 271 us), so the global heaviest-first order spreads the heads
+            kb = L / nbh;
+            bh = L % nbh;
+        } else if (CAUSAL) {
+            xcd_grouped(L, nkb, nbh, slots, kb, bh);
+        } else {
+            const int Lp = xcd_contiguous(L, nkb * nbh);
+            kb = Lp % nkb;
+            bh = Lp / nkb;
+        }
+        h = bh % gridDim.y;
+        b = bh / gridDim.y;
+    } else if (CAUSAL) {
         const int nbh = gridDim.y * gridDim.z;
         const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
         kb = L / nbh;

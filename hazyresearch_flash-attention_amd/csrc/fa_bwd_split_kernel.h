@@ -68,7 +68,7 @@ constexpr bool bwd_split_skew(bool dq, bool dropout, bool sparse) {
 
 // DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
-__global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a, const FaBlockMask bm) {
+__global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a, const FaBlockMask bm, const int slots) {
     using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL, bwd_split_skew(DQ, DROPOUT, SPARSE)>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
@@ -79,9 +79,27 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
     float *lse_s = (float *)(smem + C::OFF_LSE);
     float *del_s = (float *)(smem + C::OFF_DELTA);
 
-    // causal LPT order as in fa_bwd_kernel
+    // block order as in fa_bwd_kernel (FA_BWD_XCD: head-major per XCD, heaviest block first)
     int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    if (CAUSAL) {
+    if (FA_BWD_XCD) {
+        const int nkb = gridDim.x, nbh = gridDim.y * gridDim.z;
+        const int L = blockIdx.x + nkb * (blockIdx.y + gridDim.y * blockIdx.z);
+        int bh;
+        if (CAUSAL && DQ) {
+            // dQ by fp32 atomics: a group's key blocks would all add into the same dQ rows at
+            // once (C3: 315 vs 271 us), so the global heaviest-first order spreads the heads
+            kb = L / nbh;
+            bh = L % nbh;
+        } else if (CAUSAL) {
+            xcd_grouped(L, nkb, nbh, slots, kb, bh);
+        } else {
+            const int Lp = xcd_contiguous(L, nkb * nbh);
+            kb = Lp % nkb;
+            bh = Lp / nkb;
+        }
+        h = bh % gridDim.y;
+        b = bh / gridDim.y;
+    } else if (CAUSAL) {
         const int nbh = gridDim.y * gridDim.z;
         const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
         kb = L / nbh;

@@ -82,6 +82,42 @@ __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// XCD-aware work order. The dispatcher hands workgroup L (linear id) to XCD L & 7, and each XCD
+// takes its share in order of L >> 3; this maps L to a position Lp such that every XCD covers a
+// contiguous run of [0, nwg) (bijective for any nwg). Grids ordered head-major in Lp keep the
+// blocks of one head on one XCD at about the same time, so the rows they all stream (the
+// forward's and the dQ pass's K/V, the key-major backward's Q/dO/lse/delta) come from that XCD's
+// L2 instead of eight.
+__device__ __forceinline__ int xcd_contiguous(int L, int nwg) {
+    const int xcd = L & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+}
+
+// Causal grids (blocks of unequal work, rank 0 the heaviest): per XCD, its nbh / 8 heads in groups
+// of G, G * nblk ~ the workgroups one XCD runs at once (`slots`), heaviest-first across the group's
+// heads, groups one after the other. One group's rows fit one L2 (a head-major order alone left
+// C3's few blocks per head unbalanced; a global heaviest-first order spread ~24 heads per XCD at
+// C4: 5.5 GB fetched for 0.8 GB of Q/K/V/dO). nbh not a multiple of 8: the global order.
+__device__ __forceinline__ void xcd_grouped(int L, int nblk, int nbh, int slots, int &rank, int &bh) {
+    if ((nbh & 7) == 0) {
+        const int nh = nbh >> 3, x = L & 7, i = L >> 3;
+        int G = (slots + nblk - 1) / nblk;
+        G = G < 1 ? 1 : (G > nh ? nh : G);
+        const int per = G * nblk;
+        const int grp = i / per, w = i - grp * per;
+        const int gh = nh - grp * G < G ? nh - grp * G : G;
+        rank = w / gh;
+        bh = x * nh + grp * G + (w - rank * gh);
+    } else {
+        rank = L / nbh;
+        bh = L % nbh;
+    }
+}
+
+#ifndef FA_BWD_XCD
+#define FA_BWD_XCD 1   // 1: backward grids in xcd_contiguous head-major order (0: the round-2 orders)
+#endif
+
 // ---------------------------------------------------------------------------------------
 // LDS tile image: [rows][D] 16-bit, 16-byte chunks XOR-swizzled so that
 //   (a) ds_read_b128 row reads (lane -> row r = l&31, fixed chunk) and

@@ -111,7 +111,7 @@ constexpr int fwd_waves_per_eu(int D, int NW, bool dropout, bool sparse) {
 #define FA_FWD_BOUNDS(NW) __launch_bounds__(64 * NW)
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false, bool KSPLIT = false>
-__global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu(D, NW, DROPOUT, SPARSE)))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm) {
+__global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu(D, NW, DROPOUT, SPARSE)))) void fa_fwd_kernel(const FaFwdArgs a, const FaBlockMask bm, const int slots) {
     static_assert(!KSPLIT || (!CAUSAL && !DROPOUT && !SPARSE && NW % 2 == 0), "split-K: dense non-causal only");
     using C = FwdCfg<D, NW, KSPLIT>;
     using S = Swz<D>;
@@ -126,7 +126,12 @@ __global__ FA_FWD_BOUNDS(NW) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu
     const int nwg = nqb * nbh;
     const int L = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
     int qb, bh_lin;
-    if (CAUSAL) {
+    if (CAUSAL && FA_BWD_XCD) {
+        // heaviest (last) query blocks first within XCD head groups (xcd_grouped)
+        int rank;
+        xcd_grouped(L, nqb, nbh, slots, rank, bh_lin);
+        qb = nqb - 1 - rank;
+    } else if (CAUSAL) {
         // global LPT order: the heaviest (last) query blocks of every head first
         qb = nqb - 1 - L / nbh;
         bh_lin = L % nbh;

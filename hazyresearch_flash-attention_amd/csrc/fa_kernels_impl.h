@@ -14,6 +14,22 @@
 
 namespace fa {
 
+// Workgroups of one kernel that run at once on one XCD (occupancy per CU x CUs / 8), the `slots`
+// argument of the causal block orders (fa_common.h xcd_grouped). Called from each launcher
+// template instantiation, so the cached value is per kernel.
+// Measured (tools/ab_libs.sh, C3/C4 event times): groups of 2x the occupancy-derived slots run
+// C4's causal forward 872 vs 891 us (x1) and 935 (global order), its backward 3375 vs 3411 /
+// 3665, and C3's forward as fast as the global order (x1: +13 %)
+#ifndef FA_XCD_SLOTS_MUL
+#define FA_XCD_SLOTS_MUL 2
+#endif
+template <class K>
+static int xcd_slots_of(K kern, int threads, int lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, lds) != hipSuccess || n < 1) n = 1;
+    const int cus = device_cus();
+    return n * (cus > 0 ? cus : 256) / 8 * FA_XCD_SLOTS_MUL;
+}
 
 template <int D, typename T, bool CAUSAL, bool DROPOUT, int NW, bool SPARSE = false, bool KSPLIT = false>
 static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t stream) {
@@ -21,8 +37,9 @@ static hipError_t launch_fwd_nw(const FaFwdArgs &a, const FaBlockMask &bm, hipSt
     const int lds = C::lds_bytes(DROPOUT);
     auto kern = fa_fwd_kernel<D, T, CAUSAL, DROPOUT, NW, SPARSE, KSPLIT>;
     FA_ENSURE_LDS(kern, lds);
+    static const int slots = xcd_slots_of(kern, C::NT, lds);
     dim3 grid((a.max_seqlen_q + C::BM - 1) / C::BM, a.nheads, a.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a, bm);
+    hipLaunchKernelGGL(kern, grid, dim3(C::NT), lds, stream, a, bm, slots);
     return hipGetLastError();
 }
 
@@ -81,15 +98,17 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
                               bwd_split_skew(!DQK, DROPOUT, SPARSE)>;
         auto kern = fa_bwd_split_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
         FA_ENSURE_LDS(kern, C::LDS_BYTES);
+        static const int slots = xcd_slots_of(kern, C::NT, C::LDS_BYTES);
         dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
-        hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
+        hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm, slots);
         if constexpr (DQK) {
             constexpr int NWQ = FA_BWD_DQ_NW;
             using CQ = DqCfg<D, NWQ>;
             auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
             FA_ENSURE_LDS(kq, CQ::LDS_BYTES);
+            static const int qslots = xcd_slots_of(kq, CQ::NT, CQ::LDS_BYTES);
             dim3 gq((a.max_seqlen_q + CQ::BM - 1) / CQ::BM, a.nheads, a.batch);
-            hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a);
+            hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a, qslots);
         }
         return hipGetLastError();
     } else {
@@ -97,15 +116,17 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
         constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
         auto kern = fa_bwd_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
         FA_ENSURE_LDS(kern, C::LDS_BYTES);
+        static const int slots = xcd_slots_of(kern, C::NT, C::LDS_BYTES);
         dim3 grid((a.max_seqlen_k + C::BKV - 1) / C::BKV, a.nheads, a.batch);
-        hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm);
+        hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS_BYTES, stream, a, bm, slots);
         if constexpr (DQK) {
             constexpr int NWQ = FA_BWD_DQ_NW;
             using CQ = DqCfg<D, NWQ>;
             auto kq = fa_bwd_dq_kernel<D, T, CAUSAL, NWQ>;
             FA_ENSURE_LDS(kq, CQ::LDS_BYTES);
+            static const int qslots = xcd_slots_of(kq, CQ::NT, CQ::LDS_BYTES);
             dim3 gq((a.max_seqlen_q + CQ::BM - 1) / CQ::BM, a.nheads, a.batch);
-            hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a);
+            hipLaunchKernelGGL(kq, gq, dim3(CQ::NT), CQ::LDS_BYTES, stream, a, qslots);
         }
         return hipGetLastError();
     }
