@@ -38,6 +38,18 @@ __device__ __forceinline__ void op(uint32_t &x, uint32_t y) {
         asm volatile("v_cmp_le_u32_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:DWORD" : : "v"(x), "v"(y) : "vcc");
     } else if constexpr (OP == 11) {
         asm volatile("v_mul_f32 %0, %0, %1" : "+v"(x) : "v"(y));
+    } else if constexpr (OP == 12) {
+        asm volatile("v_exp_f16 %0, %0" : "+v"(x));
+    } else if constexpr (OP == 13) {
+        asm volatile("v_exp_f16_sdwa %0, %0 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(x));
+    } else if constexpr (OP == 14) {
+        asm volatile("v_fma_mixlo_f16 %0, %1, %1, -%0" : "+v"(x) : "v"(y));
+    } else if constexpr (OP == 15) {
+        asm volatile("v_fma_mixhi_f16 %0, %1, %1, -%0" : "+v"(x) : "v"(y));
+    } else if constexpr (OP == 16) {
+        asm volatile("v_cvt_pk_bf16_f32 %0, %0, %1" : "+v"(x) : "v"(y));
+    } else if constexpr (OP == 17) {
+        asm volatile("v_or3_b32 %0, %0, %1, %1" : "+v"(x) : "v"(y));
     }
 }
 
@@ -100,5 +112,11 @@ int main() {
     run<9>("v_mad_u32_u24", cyc, sink);
     run<10>("v_cmp_le_u32_sdwa", cyc, sink);
     run<11>("v_mul_f32", cyc, sink);
+    run<12>("v_exp_f16", cyc, sink);
+    run<13>("v_exp_f16_sdwa(hi)", cyc, sink);
+    run<14>("v_fma_mixlo_f16", cyc, sink);
+    run<15>("v_fma_mixhi_f16", cyc, sink);
+    run<16>("v_cvt_pk_bf16_f32", cyc, sink);
+    run<17>("v_or3_b32", cyc, sink);
     return 0;
 }

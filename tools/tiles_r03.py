@@ -27,6 +27,7 @@ CFGS = {
     "D128": (8, 12, 2048, 2048, 128, "bf16", False, 0.0, False),
     "C2": (8, 12, 512, 512, 64, "fp16", False, 0.0, False),
     "C3": (8, 12, 2048, 2048, 64, "bf16", True, 0.1, False),
+    "C3nd": (8, 12, 2048, 2048, 64, "bf16", True, 0.0, False),    # C3 without dropout (its cost)
     "C4": (16, 12, 4096, 4096, 128, "bf16", True, 0.0, False),
     "C5": (4, 16, 1024, 4096, 64, "bf16", False, 0.0, True),
 }
