@@ -43,7 +43,8 @@ import sys
 # ------------------------------------------------------------------------------------------
 # geometry
 # ------------------------------------------------------------------------------------------
-D = 64                 # head-dim tile (head_dim <= 64 is zero-padded by the loads)
+D = 64                 # head-dim tile: 64 (head_dim in (32, 64], zero-padded by the loads) or 128
+                       # (head_dim == 128); configure() sets the dependent constants and registers
 BN = 64                # keys per tile
 R = 4                  # LDS ring slots (K and V each)
 DIST = 3               # DMA prefetch distance in tiles (tile t issues K(t+1+DIST), V(t+DIST))
@@ -73,6 +74,12 @@ def set_geometry(r, dist):
     U = r * 2 // math.gcd(r, 2)
     VREG = R * TILE
     LDS_BYTES = 2 * R * TILE
+NKS = D // 16          # 16-deep k-steps of Q K^T
+NDT = D // 32          # 32-wide d-blocks of O^T
+NP = D // 32           # 1-KiB LDS-DMA pieces per tensor, tile and wave
+ROWB = 2 * D           # bytes per LDS image row
+KFB = D // 2           # registers of one K (or V^T) fragment buffer per wave
+NBK = NBV = 2          # K / V^T fragment buffers (double-buffered at D = 64)
 RESCALE_THR = 8.0      # log2-domain threshold of the deferred rescale (fa_fwd_kernel.h)
 OOB = 0x80000000
 PROBE = set()          # timing-only variants (tools/asm_variants.py); empty in the product build
@@ -105,6 +112,72 @@ A_Q = {'A': 76, 'B': 92}        # Q fragments (B operand of S^T = K Q^T), 4 k-st
 A_KF = 108                      # K fragments [buf 2][st*4+ks] x 4
 A_VF = 172                      # V^T fragments [buf 2][dt*4+st*2+s] x 4
 NAGPR = 236
+O_BASE = False         # Q loads / O stores from one row base + immediates (requires head_dim == D)
+QL_VGPR = False        # Q fragments, row sums and the 0/1 indicator in VGPRs (D = 128: AGPRs hold
+#                        O, K and V^T fragments, 256, the most an AGPR index reaches)
+
+
+def rq(base):
+    """Text and register names of a 4-register Q / row-sum / indicator operand."""
+    return vs(base, 4) if QL_VGPR else as_(base, 4)
+
+
+def rqn(base, n=4):
+    return rv(base, n) if QL_VGPR else ra(base, n)
+
+
+def configure(hd):
+    """Head-dim tile. 64: the layout above (head_dim in (32, 64]). 128 (head_dim == 128): twice the
+    k-steps and d-blocks, single K / V^T fragment buffers (the K reads of tile j+1 follow the last
+    QK_B(j) MFMA, the V^T reads of tile j follow PV_B(j-1), one phase earlier), Q / O offsets as
+    one base + immediates, 128 KiB of LDS ring. 248 VGPRs (Q, row sums, indicator among them) + 256
+    AGPRs (O, K and V^T fragments)."""
+    global D, NKS, NDT, NP, ROWB, KFB, NBK, NBV, TILE, VREG, LDS_BYTES, O_BASE, VREADS_P1, QL_VGPR
+    global V_KADDR, V_VADDR, V_DMA, V_S, V_P, V_MTHR, V_MC, V_TMP, V_BPA, V_BPL, V_NEGINF, V_NVREL
+    global V_OOFF, V_LOFF, V_ONEF, V_LANE, V_ETMP, V_MCB, NVGPR, A_O, A_L, A_ONES, A_Q, A_KF, A_VF, NAGPR
+    assert hd in (64, 128)
+    globals().update(_D64)   # the D = 64 layout, then the D = 128 changes
+    if hd == 64:
+        return
+    D, NKS, NDT, NP, ROWB, KFB = hd, hd // 16, hd // 32, hd // 32, 2 * hd, hd // 2
+    NBK = NBV = 1
+    O_BASE, VREADS_P1, QL_VGPR = True, False, True
+    TILE = BN * D * 2
+    VREG = R * TILE
+    LDS_BYTES = 2 * R * TILE
+    # S / P first: the prologue's temporaries (v16..v51) live there until QK_A(0)
+    V_S, V_P = {'A': 4, 'B': 36}, {'A': 68, 'B': 84}
+    V_KADDR, V_VADDR, V_DMA = 100, 108, 116
+    V_MTHR, V_MC, V_TMP = {'A': 124, 'B': 125}, {'A': 126, 'B': 127}, {'A': 128, 'B': 136}
+    V_BPA, V_BPL, V_NEGINF, V_NVREL = 144, 145, 146, 147
+    V_OOFF, V_LOFF = {'A': 148, 'B': 149}, {'A': 150, 'B': 151}
+    V_ONEF, V_LANE, V_ETMP = 152, 153, 154
+    # VGPRs: Q fragments, row sums and the indicator after the exp temporaries (A_* names kept)
+    A_Q, A_L, A_ONES = {'A': 172, 'B': 204}, {'A': 236, 'B': 240}, 244
+    V_MCB = {'A': 248, 'B': 252}
+    NVGPR = 248
+    A_O, A_KF, A_VF = {'A': 0, 'B': 64}, 128, 192
+    NAGPR = 256
+
+
+_D64 = {k: (dict(v) if isinstance(v, dict) else v) for k, v in globals().items()
+        if k in ('D', 'NKS', 'NDT', 'NP', 'ROWB', 'KFB', 'NBK', 'NBV', 'TILE', 'VREG', 'LDS_BYTES', 'O_BASE',
+                 'VREADS_P1', 'QL_VGPR', 'V_KADDR', 'V_VADDR', 'V_DMA', 'V_S', 'V_P', 'V_MTHR', 'V_MC', 'V_TMP',
+                 'V_BPA', 'V_BPL', 'V_NEGINF', 'V_NVREL', 'V_OOFF', 'V_LOFF', 'V_ONEF', 'V_LANE', 'V_ETMP',
+                 'V_MCB', 'NVGPR', 'A_O', 'A_L', 'A_ONES', 'A_Q', 'A_KF', 'A_VF', 'NAGPR')}
+
+
+def epi_regs(X, idx):
+    """Epilogue temporaries of block X, output slot idx (d-block, group): 8 fp32 and 4 packed
+    words in registers dead by then. D = 64: S_X and P_X. D = 128 (8 slots): S_A..S_B for the fp32
+    (both softmaxes are done); the words of block A in P_A then the exp temporaries (P_B still
+    feeds the last P_B.V beside it), of block B in P_A..P_B."""
+    if D == 64:
+        return V_S[X] + 8 * idx, V_P[X] + 4 * idx
+    E = V_S['A'] + 8 * idx
+    if X == 'A' and idx >= 4:
+        return E, V_ETMP + 4 * (idx - 4)
+    return E, V_P['A'] + 4 * idx
 
 # ---- SGPRs
 S_KD, S_VD, S_QD, S_OD, S_LD = 8, 12, 16, 20, 24   # buffer descriptors (4 each)
@@ -126,13 +199,16 @@ class Inst:
     cost: issue cycles used by the gap placer. rd / wr: register names ('v12', 'a40', 's3',
     'vcc', 'm0'). rdc: MFMA srcC registers. pipe: MFMA pipe cycles (32 or 16).
     deadline: index of the MFMA (within its phase) that this filler must precede.
+    not_before: number of the phase's MFMAs that must be issued before this filler (it overwrites
+    their operands: the single-buffered fragments at D = 128).
     """
-    __slots__ = ('txt', 'kind', 'cost', 'rd', 'wr', 'rdc', 'pipe', 'deadline', 'lgkm_dst')
+    __slots__ = ('txt', 'kind', 'cost', 'rd', 'wr', 'rdc', 'pipe', 'deadline', 'lgkm_dst', 'not_before')
 
     def __init__(self, txt, kind, cost=4, rd=(), wr=(), rdc=(), pipe=0, deadline=None):
         self.txt, self.kind, self.cost = txt, kind, cost
         self.rd, self.wr, self.rdc = frozenset(rd), frozenset(wr), frozenset(rdc)
         self.pipe, self.deadline = pipe, deadline
+        self.not_before = None
 
 
 def rv(base, n=1):
@@ -181,7 +257,7 @@ class Gen:
         self.cvt = 'v_cvt_pk_bf16_f32' if dtype == 'bf16' else 'v_cvt_pk_f16_f32'
         self.one2 = 0x3F803F80 if dtype == 'bf16' else 0x3C003C00
         self.nlabel = 0
-        self.name = f'fa_fwd_d64_{dtype}_asm'
+        self.name = f'fa_fwd_d{D}_{dtype}_asm'
 
     def lab(self, stem):
         self.nlabel += 1
@@ -194,11 +270,11 @@ class Gen:
         S, Q = V_S[X], A_Q[X]
         for st in range(2):
             acc = S + 16 * st
-            for ks in range(4):
-                kf = A_KF + 32 * (t % 2) + 4 * (st * 4 + ks)
+            for ks in range(NKS):
+                kf = A_KF + KFB * (t % NBK) + 4 * (st * NKS + ks)
                 c = '0' if ks == 0 else vs(acc, 16)
-                out.append(Inst(f'{self.mf32} {vs(acc, 16)}, {as_(kf, 4)}, {as_(Q + 4 * ks, 4)}, {c}', 'mfma', 8,
-                                rd=ra(kf, 4) + ra(Q + 4 * ks, 4), wr=rv(acc, 16),
+                out.append(Inst(f'{self.mf32} {vs(acc, 16)}, {as_(kf, 4)}, {rq(Q + 4 * ks)}, {c}', 'mfma', 8,
+                                rd=ra(kf, 4) + rqn(Q + 4 * ks), wr=rv(acc, 16),
                                 rdc=rv(acc, 16) if ks else (), pipe=32))
         return out
 
@@ -211,14 +287,14 @@ class Gen:
         for st in range(2):
             for s in range(2):
                 p = P + 4 * (st * 2 + s)
-                sums.append(Inst(f'{self.mf16} {as_(L, 4)}, {as_(A_ONES, 4)}, {vs(p, 4)}, {as_(L, 4)}', 'mfma', 8,
-                                 rd=ra(A_ONES, 4) + rv(p, 4), wr=ra(L, 4), rdc=ra(L, 4), pipe=16))
+                sums.append(Inst(f'{self.mf16} {rq(L)}, {rq(A_ONES)}, {vs(p, 4)}, {rq(L)}', 'mfma', 8,
+                                 rd=rqn(A_ONES) + rv(p, 4), wr=rqn(L), rdc=rqn(L), pipe=16))
         si = 0
-        for dt in range(2):
+        for dt in range(NDT):
             for st in range(2):
                 for s in range(2):
                     f = dt * 4 + st * 2 + s
-                    vf = A_VF + 32 * (t % 2) + 4 * f
+                    vf = A_VF + KFB * (t % NBV) + 4 * f
                     p = P + 4 * (st * 2 + s)
                     acc = O + 16 * dt
                     use[f] = len(out)
@@ -237,9 +313,9 @@ class Gen:
             return out
         slot = KREG + (t % R) * TILE
         for st in range(2):
-            for ks in range(4):
-                kf = A_KF + 32 * (t % 2) + 4 * (st * 4 + ks)
-                out.append(Inst(f'ds_read_b128 {as_(kf, 4)}, v{V_KADDR + ks} offset:{slot + st * 4096}', 'ds', 2,
+            for ks in range(NKS):
+                kf = A_KF + KFB * (t % NBK) + 4 * (st * NKS + ks)
+                out.append(Inst(f'ds_read_b128 {as_(kf, 4)}, v{V_KADDR + ks} offset:{slot + st * 32 * ROWB}', 'ds', 2,
                                 rd=[f'v{V_KADDR + ks}'], wr=ra(kf, 4)))
         return out
 
@@ -250,14 +326,14 @@ class Gen:
         if 'nolds' in PROBE:
             return out
         slot = VREG + (t % R) * TILE
-        for dt in range(2):
+        for dt in range(NDT):
             for st in range(2):
                 for s in range(2):
                     f = dt * 4 + st * 2 + s
-                    vf = A_VF + 32 * (t % 2) + 4 * f
+                    vf = A_VF + KFB * (t % NBV) + 4 * f
                     for half in range(2):
                         addr = V_VADDR + dt * 2 + half
-                        off = slot - VREG + (32 * st + 16 * s) * 128   # VREG is in the address VGPR
+                        off = slot - VREG + (32 * st + 16 * s) * ROWB   # VREG is in the address VGPR
                         out.append((f, Inst(f'ds_read_b64_tr_b16 {as_(vf + 2 * half, 2)}, v{addr} offset:{off}', 'ds', 2,
                                             rd=[f'v{addr}'], wr=ra(vf + 2 * half, 2))))
         return out
@@ -286,9 +362,9 @@ class Gen:
             out.append(salu(f's_addc_u32 s{desc + 1}, s{desc + 1}, 0', rd=[dregs[1], 'scc'], wr=[dregs[1], 'scc']))
             out.append(salu(f's_sub_u32 s{desc + 2}, s{desc + 2}, {st}', rd=[dregs[2], st], wr=[dregs[2], 'scc']))
             out.append(salu(f's_cselect_b32 s{desc + 2}, 0, s{desc + 2}', rd=[dregs[2], 'scc'], wr=[dregs[2]]))
-        for i in range(2):
+        for i in range(NP):
             m0 = region + (t % R) * TILE + 4096 * i   # + 1024 * wave (S_M0B)
-            voff = V_DMA + (0 if kind == 'K' else 2) + i
+            voff = V_DMA + (0 if kind == 'K' else NP) + i
             out.append(Inst(f's_add_u32 m0, s{S_M0B}, {m0}', 'm0', 2, rd=[f's{S_M0B}'], wr=['m0', 'scc']))
             out.append(Inst(f'buffer_load_dwordx4 v{voff}, s[{desc}:{desc + 3}], 0 offen lds', 'dma', 16,
                             rd=[f'v{voff}', 'm0'] + dregs))
@@ -383,7 +459,7 @@ class Gen:
             # max ops spread over the first 70 % of the exp stream
             out += merge(ex, [(i, x) for i, x in zip(spread(len(mx), 2, int(len(ex) * 0.7)), mx)])
         resc, ret = self.lab(f'resc{X}'), self.lab(f'ret{X}')
-        touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], 32) + ra(A_L[X], 4) + rv(V_ETMP, 16) + rv(P, 16)
+        touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], D // 2) + rqn(A_L[X]) + rv(V_ETMP, 16) + rv(P, 16)
         if MC_BANKS:
             touched += rv(V_MCB[X], 4)
         out.append(Inst(f's_cbranch_vccnz {resc}\n{ret}:', 'br', 4, rd=['vcc'] + touched, wr=touched))
@@ -443,7 +519,7 @@ class Gen:
         # branch and its return label form one unbreakable group
         # (it also carries the registers the out-of-line block touches, so the scheduler keeps
         # their readers after it and anything unrelated may move across it)
-        touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], 32) + ra(A_L[X], 4)
+        touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], D // 2) + rqn(A_L[X])
         out.append(Inst(f's_cbranch_vccnz {resc}\n{ret}:', 'br', 4, rd=['vcc'] + touched, wr=touched))
         rescue.append(self.rescale_block(X, resc, ret))
         # exp2(s * c - m * c), converted pairwise into the 16-bit P operand
@@ -537,7 +613,7 @@ class Gen:
         b = []
         if MC_BANKS:
             b += [V(f'v_mov_b32 v{c}, v{mc}', c, [mc]) for c in range(V_MCB[X], V_MCB[X] + 4)]
-        for r in range(32):
+        for r in range(D // 2):
             t = T + 2 + (r % 4)
             b.append(Inst(f'v_accvgpr_read_b32 v{t}, a{O + r}', 'accr', rd=[f'a{O + r}'], wr=[f'v{t}']))
             b.append(V(f'v_mul_f32 v{t}, v{t}, v{T}', t, [t, T]))
@@ -545,6 +621,9 @@ class Gen:
         b.append(Inst(f'ds_bpermute_b32 v{T + 1}, v{V_BPA}, v{T}', 'ds', 2, rd=[f'v{V_BPA}', f'v{T}'], wr=[f'v{T + 1}']))
         for r in range(4):
             t = T + 2 + r
+            if QL_VGPR:
+                b.append(V(f'v_mul_f32 v{L + r}, v{L + r}, v{T + 1}', L + r, [L + r, T + 1]))
+                continue
             b.append(Inst(f'v_accvgpr_read_b32 v{t}, a{L + r}', 'accr', rd=[f'a{L + r}'], wr=[f'v{t}']))
             b.append(V(f'v_mul_f32 v{t}, v{t}, v{T + 1}', t, [t, T + 1]))
             b.append(Inst(f'v_accvgpr_write_b32 a{L + r}, v{t}', 'accw', rd=[f'v{t}'], wr=[f'a{L + r}']))
@@ -557,7 +636,10 @@ class Gen:
         S, T, mc = V_S[X], V_TMP[X], V_MC[X]
         O, L = A_O[X], A_L[X]
         e = []
-        e.append(Inst(f'v_accvgpr_read_b32 v{T}, a{L}', 'accr', rd=[f'a{L}'], wr=[f'v{T}']))
+        if QL_VGPR:
+            e.append(V(f'v_mov_b32 v{T}, v{L}', T, [L]))
+        else:
+            e.append(Inst(f'v_accvgpr_read_b32 v{T}, a{L}', 'accr', rd=[f'a{L}'], wr=[f'v{T}']))
         e.append(Inst(f'ds_bpermute_b32 v{T + 1}, v{V_BPL}, v{T}', 'ds', 2, rd=[f'v{V_BPL}', f'v{T}'], wr=[f'v{T + 1}']))
         e.append(V(f'v_rcp_f32 v{T + 2}, v{T + 1}', T + 2, [T + 1], kind='trans', cost=8))
         e.append(V(f'v_cmp_nlg_f32 vcc, 0, v{T + 1}', 'vcc', [T + 1]))
@@ -570,12 +652,11 @@ class Gen:
                       wr=[f'v{T + 3}']))
         e.append(Inst(f'buffer_store_dword v{T + 3}, v{V_LOFF[X]}, s[{S_LD}:{S_LD + 3}], 0 offen', 'vstore', 8,
                       rd=[f'v{T + 3}', f'v{V_LOFF[X]}']))
-        for dt in range(2):
+        for dt in range(NDT):
             for gi, g in enumerate((0, 2)):
                 # registers 4g..4g+7 of d-block dt hold d = 8g + 4hi + 0..3 and 8(g+1) + 4hi + 0..3
                 base = O + 16 * dt + 4 * g
-                E = S + (dt * 2 + gi) * 8          # 8 fp32 temps (S_X is dead by now)
-                Wb = V_P[X] + 4 * (dt * 2 + gi)    # 4 packed words (P_X is dead by now)
+                E, Wb = epi_regs(X, dt * 2 + gi)   # 8 fp32 temps, 4 packed words (dead registers)
                 for k in range(8):
                     e.append(Inst(f'v_accvgpr_read_b32 v{E + k}, a{base + k}', 'accr', rd=[f'a{base + k}'],
                                   wr=[f'v{E + k}']))
@@ -591,21 +672,33 @@ class Gen:
                               wr=[f'v{Wb}', f'v{Wb + 2}']))
                 e.append(Inst(f'v_permlane32_swap_b32 v{Wb + 1}, v{Wb + 3}', 'perm', 4, rd=[f'v{Wb + 1}', f'v{Wb + 3}'],
                               wr=[f'v{Wb + 1}', f'v{Wb + 3}']))
-                e.append(Inst(f'buffer_store_dwordx4 {vs(Wb, 4)}, v{V_OOFF[X] + dt * 2 + gi}, s[{S_OD}:{S_OD + 3}], 0 offen',
-                              'vstore', 8, rd=rv(Wb, 4) + [f'v{V_OOFF[X] + dt * 2 + gi}']))
+                if O_BASE:   # one row base + immediate (head_dim == D)
+                    oreg, oimm = V_OOFF[X], f' offset:{16 * (4 * dt + g)}'
+                else:
+                    oreg, oimm = V_OOFF[X] + dt * 2 + gi, ''
+                e.append(Inst(f'buffer_store_dwordx4 {vs(Wb, 4)}, v{oreg}, s[{S_OD}:{S_OD + 3}], 0 offen{oimm}',
+                              'vstore', 8, rd=rv(Wb, 4) + [f'v{oreg}']))
         return e
 
     # ------------------------------------------------------------------ phases
     def phase1(self, t, masked=False, last=False, rescue=None):
         """Tile t, phase 1: QK_B(t) + PV_B(t-1) + row sums beside block A's softmax of tile t,
         K(t+1) fragment reads and the K(t+1+DIST) DMA."""
-        mf = self.qk('B', t) + self.pv_sum('B', t - 1)[0]
+        qkb = self.qk('B', t)
+        mf = qkb + self.pv_sum('B', t - 1)[0]
         sm = self.softmax('A', masked, rescue)
         side = [] if last else self.kreads(t + 1)
+        k_lo = 16
+        if NBK == 1:
+            # one K buffer: the reads of K(t+1) overwrite what QK_B(t) reads; they go behind its
+            # last MFMA, in the part of the softmax stream that lands there
+            for x in side:
+                x.not_before = len(qkb)
+            k_lo = len(sm) * sum(m.pipe for m in qkb) // sum(m.pipe for m in mf) + 2
         if VREADS_P1:
             side = [x for _, x in self.vreads(t)] + side
         dma = [] if (last or DMA_P2) else self.dma('K', t + 1 + DIST)
-        fill = merge(sm, [(i, x) for i, x in zip(spread(len(side), 16, len(sm) - 4), side)] +
+        fill = merge(sm, [(i, x) for i, x in zip(spread(len(side), k_lo, len(sm) - 4), side)] +
                      [(i, x) for i, x in zip(spread(len(dma), 6, len(sm) - 10), dma)])
         return [mark()] + place(mf, fill)
 
@@ -702,6 +795,9 @@ def place(mfmas, fillers, window=10):
         take = 0
         a2 = acc
         while take < len(rest) and (take <= forced or a2 + rest[take].cost * 0.5 <= target):
+            nb = rest[take].not_before
+            if nb is not None and nb > g + 1:
+                break     # must follow MFMA nb-1 (not issued yet): in-order stream waits
             a2 += rest[take].cost
             take += 1
         chunk, rest = rest[:take], rest[take:]
@@ -931,8 +1027,10 @@ def S(txt, rd=(), wr=(), kind='salu'):
 
 
 def xfun(dst, r, t1, t2):
-    """x(r) of the D=64 LDS swizzle (fa_common.h Swz<64>): u = (r>>1)&7, x = ((u&1)<<2)|(u>>1)."""
-    return [V(f'v_bfe_u32 v{t1}, v{r}, 1, 1', t1, [r]),
+    """x(r) of the LDS swizzle (fa_common.h Swz<D>): D = 64: u = (r>>1)&7, x = ((u&1)<<2)|(u>>1);
+    D = 128: x = ((r&3)<<2)|((r>>2)&3)."""
+    lo = (1, 1) if D == 64 else (0, 2)
+    return [V(f'v_bfe_u32 v{t1}, v{r}, {lo[0]}, {lo[1]}', t1, [r]),
             V(f'v_lshlrev_b32 v{t1}, 2, v{t1}', t1, [t1]),
             V(f'v_bfe_u32 v{t2}, v{r}, 2, 2', t2, [r]),
             V(f'v_or_b32 v{dst}, v{t1}, v{t2}', dst, [t1, t2])]
@@ -1021,50 +1119,60 @@ def prologue(g):
           V('v_bfe_u32 v17, v0, 5, 1', 17, [0]), V('v_bfe_u32 v18, v0, 2, 2', 18, [0]),
           V('v_and_b32 v19, 3, v0', 19, [0]), V('v_bfe_u32 v20, v0, 4, 1', 20, [0])]
     p += xfun(21, 16, 22, 23)
-    for ks in range(4):   # K fragment reads: row l32, chunk 2ks + hi
+    rsh = ROWB.bit_length() - 1     # log2 of the LDS row bytes
+    for ks in range(NKS):   # K fragment reads: row l32, chunk 2ks + hi
         p += [V(f'v_add_u32 v22, {2 * ks}, v17', 22, [17]), V('v_xor_b32 v22, v22, v21', 22, [22, 21]),
-              V('v_lshlrev_b32 v22, 4, v22', 22, [22]), V(f'v_lshl_add_u32 v{V_KADDR + ks}, v16, 7, v22', V_KADDR + ks, [16, 22])]
+              V('v_lshlrev_b32 v22, 4, v22', 22, [22]), V(f'v_lshl_add_u32 v{V_KADDR + ks}, v16, {rsh}, v22', V_KADDR + ks, [16, 22])]
     # V^T tr reads: row 4hi + qq + 8 half, column 32 dt + 16 grp + 4 pp
     p += [V('v_lshl_add_u32 v24, v17, 2, v18', 24, [17, 18]), V('v_lshrrev_b32 v25, 1, v19', 25, [19]),
           V('v_lshl_add_u32 v25, v20, 1, v25', 25, [20, 25]), V('v_and_b32 v26, 1, v19', 26, [19]),
           V('v_lshlrev_b32 v26, 3, v26', 26, [26])]
     for half in range(2):
         p += [V(f'v_add_u32 v27, {8 * half}, v24', 27, [24])] + xfun(28, 27, 29, 30)
-        for dt in range(2):
+        for dt in range(NDT):
             p += [V(f'v_add_u32 v29, {4 * dt}, v25', 29, [25]), V('v_xor_b32 v29, v29, v28', 29, [29, 28]),
                   V('v_lshl_or_b32 v29, v29, 4, v26', 29, [29, 26]),
-                  V(f'v_lshl_add_u32 v{V_VADDR + dt * 2 + half}, v27, 7, v29', V_VADDR + dt * 2 + half, [27, 29]),
+                  V(f'v_lshl_add_u32 v{V_VADDR + dt * 2 + half}, v27, {rsh}, v29', V_VADDR + dt * 2 + half, [27, 29]),
                   V(f'v_add_u32 v{V_VADDR + dt * 2 + half}, {VREG}, v{V_VADDR + dt * 2 + half}',
                     V_VADDR + dt * 2 + half, [V_VADDR + dt * 2 + half])]
     p += [V(f'v_mov_b32 v{V_NEGINF}, 0xff800000', V_NEGINF, []), V(f'v_mov_b32 v{V_ONEF}, 1.0', V_ONEF, []),
           V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
-    # DMA source offsets: pieces `wave` and `wave + 4` of a tile; lane l -> row 8p + l/8, slot l%8
-    p += [V(f'v_lshrrev_b32 v33, 3, v{L}', 33, [L]), V(f'v_and_b32 v34, 7, v{L}', 34, [L]),
-          S(f's_lshl_b32 s91, s{S_WAVE}, 3')]
-    for i in range(2):
-        p += [S(f's_add_u32 s92, s91, {32 * i}'), V('v_add_u32 v35, s92, v33', 35, [33])]
+    # DMA source offsets: pieces `wave + 4i` of a tile; lane l -> row RPP p + l/LPR, slot l%LPR
+    # (RPP = rows per 1-KiB piece, LPR = 16-B chunks per row)
+    lpr = D // 8
+    rpp = 1024 // ROWB
+    p += [V(f'v_lshrrev_b32 v33, {lpr.bit_length() - 1}, v{L}', 33, [L]), V(f'v_and_b32 v34, {lpr - 1}, v{L}', 34, [L]),
+          S(f's_lshl_b32 s91, s{S_WAVE}, {rpp.bit_length() - 1}')]
+    for i in range(NP):
+        p += [S(f's_add_u32 s92, s91, {4 * rpp * i}'), V('v_add_u32 v35, s92, v33', 35, [33])]
         p += xfun(36, 35, 37, 38)
         p += [V('v_xor_b32 v36, v34, v36', 36, [34, 36]), V('v_lshlrev_b32 v37, 3, v36', 37, [36]),
               V('v_cmp_gt_u32 vcc, s74, v37', 'vcc', [37]),
               V('v_mul_lo_u32 v38, v35, s63', 38, [35]), V('v_lshl_add_u32 v38, v36, 4, v38', 38, [36, 38]),
               Inst(f'v_cndmask_b32 v{V_DMA + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'], wr=[f'v{V_DMA + i}']),
               V('v_mul_lo_u32 v38, v35, s64', 38, [35]), V('v_lshl_add_u32 v38, v36, 4, v38', 38, [36, 38]),
-              Inst(f'v_cndmask_b32 v{V_DMA + 2 + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'],
-                   wr=[f'v{V_DMA + 2 + i}'])]
+              Inst(f'v_cndmask_b32 v{V_DMA + NP + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'],
+                   wr=[f'v{V_DMA + NP + i}'])]
     # Q load offsets (v43..v50), O store offsets, LSE offsets of blocks A (rows +0) and B (+32)
     p += [S(f's_lshl_b32 s93, s{S_WAVE}, 6'), S('s_add_u32 s93, s93, s90')]
-    qoff = {'A': 43, 'B': 47}
+    # (O_BASE, head_dim == D: one row base per block, the chunk offsets as immediates)
+    qoff = {'A': 43, 'B': 47} if not O_BASE else {'A': V_P['A'], 'B': V_P['A'] + 1}
     for X, xo in (('A', 0), ('B', 32)):
         p += [V('v_add_u32 v39, s93, v16', 39, [16])]
         if xo:
             p += [V(f'v_add_u32 v39, {xo}, v39', 39, [39])]
-        for ks in range(4):
+        if O_BASE:
+            p += [V('v_mul_lo_u32 v42, v39, s62', 42, [39]),
+                  V(f'v_lshl_add_u32 v{qoff[X]}, v17, 4, v42', qoff[X], [17, 42]),
+                  V('v_mul_lo_u32 v42, v39, s65', 42, [39]),
+                  V(f'v_lshl_add_u32 v{V_OOFF[X]}, v17, 4, v42', V_OOFF[X], [17, 42])]
+        for ks in ([] if O_BASE else range(NKS)):
             p += [V(f'v_add_u32 v40, {2 * ks}, v17', 40, [17]), V('v_lshlrev_b32 v41, 3, v40', 41, [40]),
                   V('v_cmp_gt_u32 vcc, s74, v41', 'vcc', [41]),
                   V('v_mul_lo_u32 v42, v39, s62', 42, [39]), V('v_lshl_add_u32 v42, v40, 4, v42', 42, [40, 42]),
                   Inst(f'v_cndmask_b32 v{qoff[X] + ks}, v31, v42, vcc', 'valu', rd=['v31', 'v42', 'vcc'],
                        wr=[f'v{qoff[X] + ks}'])]
-        for dt in range(2):
+        for dt in ([] if O_BASE else range(NDT)):
             for gi, gg in enumerate((0, 2)):
                 p += [V(f'v_add_u32 v40, {4 * dt + gg}, v17', 40, [17]), V('v_lshlrev_b32 v41, 3, v40', 41, [40]),
                       V('v_cmp_gt_u32 vcc, s74, v41', 'vcc', [41]),
@@ -1082,21 +1190,31 @@ def prologue(g):
           V(f'v_bfe_u32 v41, v{L}, 4, 1', 41, [L]), V(f'v_bfe_u32 v42, v{L}, 3, 1', 42, [L]),
           V('v_cmp_eq_u32 vcc, v41, v42', 'vcc', [41, 42]), V(f'v_mov_b32 v51, {g.one2:#x}', 51, []),
           Inst('v_cndmask_b32 v51, v32, v51, vcc', 'valu', rd=['v32', 'v51', 'vcc'], wr=['v51'])]
-    p += [Inst(f'v_accvgpr_write_b32 a{A_ONES + r}, v51', 'accw', rd=['v51'], wr=[f'a{A_ONES + r}']) for r in range(4)]
+    if QL_VGPR:
+        p += [V(f'v_mov_b32 v{A_ONES + r}, v51', A_ONES + r, [51]) for r in range(4)]
+    else:
+        p += [Inst(f'v_accvgpr_write_b32 a{A_ONES + r}, v51', 'accw', rd=['v51'], wr=[f'a{A_ONES + r}']) for r in range(4)]
     # Q fragments
     for X in 'AB':
-        for ks in range(4):
+        for ks in range(NKS):
             q = A_Q[X] + 4 * ks
-            p.append(Inst(f'buffer_load_dwordx4 {as_(q, 4)}, v{qoff[X] + ks}, s[{S_QD}:{S_QD + 3}], 0 offen', 'vload', 8,
-                          rd=[f'v{qoff[X] + ks}'], wr=ra(q, 4)))
+            qr, qi = (qoff[X], f' offset:{32 * ks}') if O_BASE else (qoff[X] + ks, '')
+            p.append(Inst(f'buffer_load_dwordx4 {rq(q)}, v{qr}, s[{S_QD}:{S_QD + 3}], 0 offen{qi}', 'vload', 8,
+                          rd=[f'v{qr}'], wr=rqn(q)))
     # first DMAs: K0, [K1 V0], [K2 V1], [K3 V2] (tile t of the loop issues K(t+1+DIST), V(t+DIST))
     p += g.dma('K', 0)
     for t in range(DIST):
         p += g.dma('K', t + 1) + g.dma('V', t)
-    # zero O, row sums, V fragment buffer 1 and P_B (PV_B(-1) of tile 0 adds nothing); m = -inf
-    p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(72)]
-    p += [Inst(f'v_accvgpr_write_b32 a{A_VF + 32 + r}, v32', 'accw', rd=['v32'], wr=[f'a{A_VF + 32 + r}'])
-          for r in range(32)]
+    # zero O, row sums, the V fragment buffer PV_B(-1) reads and P_B (PV_B(-1) of tile 0 adds
+    # nothing); m = -inf
+    if QL_VGPR:
+        p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(D)]
+        p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(A_L['A'], A_L['B'] + 4)]
+    else:
+        p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(A_ONES)]
+    vf1 = A_VF + KFB * ((-1) % NBV)
+    p += [Inst(f'v_accvgpr_write_b32 a{vf1 + r}, v32', 'accw', rd=['v32'], wr=[f'a{vf1 + r}'])
+          for r in range(KFB)]
     p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
     p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in (V_MTHR['A'], V_MTHR['B'], V_MC['A'], V_MC['B'])]
     if MC_BANKS:
@@ -1284,6 +1402,7 @@ def expand_regs(spec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f16'])
+    ap.add_argument('--hd', type=int, default=64, choices=[64, 128], help='head-dim tile')
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats', action='store_true')
     ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')
@@ -1303,6 +1422,7 @@ def main():
         pt, regs = args.dump.split(':')
         DUMP = (pt, expand_regs(regs))
     PROBE.update(x for x in args.probe.split(',') if x)
+    configure(args.hd)
     global VREADS_P1, SM_PIPE
     if args.ring or args.dist:
         set_geometry(args.ring or R, args.dist or DIST)

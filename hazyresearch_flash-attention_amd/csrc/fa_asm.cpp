@@ -5,8 +5,8 @@
 // loaded per device on first use with hipModuleLoadData and launched with hipModuleLaunchKernel
 // on the caller's stream (so it is captured into hipGraphs like the HIP kernels).
 //
-// It serves the north-star shape class: head_dim in (32, 64] (the D=64 tile), fp16/bf16,
-// non-causal, no dropout, dense (no block mask), no fused rotary. Everything else keeps the HIP
+// It serves the north-star shape class: head_dim in (32, 64] (the D=64 tile) or 128 (the D=128
+// tile), fp16/bf16, non-causal, no dropout, dense (no block mask), no fused rotary. Everything else keeps the HIP
 // kernels of fa_fwd_kernel.h. Semantics are the same: var-len sequences through cu_seqlens,
 // rows past a sequence neither read nor written, LSE = m*scale + ln(sum) (-inf for no keys).
 #include <hip/hip_runtime.h>
@@ -22,6 +22,10 @@ extern const unsigned char fa_asm_fwd_d64_bf16[];
 extern const unsigned long fa_asm_fwd_d64_bf16_size;
 extern const unsigned char fa_asm_fwd_d64_f16[];
 extern const unsigned long fa_asm_fwd_d64_f16_size;
+extern const unsigned char fa_asm_fwd_d128_bf16[];
+extern const unsigned long fa_asm_fwd_d128_bf16_size;
+extern const unsigned char fa_asm_fwd_d128_f16[];
+extern const unsigned long fa_asm_fwd_d128_f16_size;
 }
 
 namespace fa {
@@ -56,24 +60,29 @@ constexpr int kRows = 256;            // query rows per workgroup
 constexpr int kMaxDev = 64;
 constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
 
+// kernels: [d-tile (0: 64, 1: 128) * 2 + dtype (0: bf16, 1: f16)]
 struct DevFns {
-    hipModule_t mod[2] = {nullptr, nullptr};
-    hipFunction_t fn[2] = {nullptr, nullptr};
+    hipModule_t mod[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipFunction_t fn[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 std::mutex g_mu;
 DevFns g_fns[kMaxDev];
 
-hipError_t get_function(int dtype, hipFunction_t *out) {
+hipError_t get_function(int dtype, int hd, hipFunction_t *out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
-    const int k = dtype == FA_DTYPE_BF16 ? 0 : 1;
+    const int k = (hd == 128 ? 2 : 0) + (dtype == FA_DTYPE_BF16 ? 0 : 1);
     std::lock_guard<std::mutex> lk(g_mu);
     DevFns &d = g_fns[dev];
     if (!d.fn[k]) {
-        const void *img = k == 0 ? (const void *)fa_asm_fwd_d64_bf16 : (const void *)fa_asm_fwd_d64_f16;
-        const char *name = k == 0 ? "fa_fwd_d64_bf16_asm" : "fa_fwd_d64_f16_asm";
+        static const void *const imgs[4] = {fa_asm_fwd_d64_bf16, fa_asm_fwd_d64_f16, fa_asm_fwd_d128_bf16,
+                                            fa_asm_fwd_d128_f16};
+        static const char *const names[4] = {"fa_fwd_d64_bf16_asm", "fa_fwd_d64_f16_asm", "fa_fwd_d128_bf16_asm",
+                                             "fa_fwd_d128_f16_asm"};
+        const void *img = imgs[k];
+        const char *name = names[k];
         e = hipModuleLoadData(&d.mod[k], img);
         if (e != hipSuccess) return e;
         e = hipModuleGetFunction(&d.fn[k], d.mod[k], name);
@@ -93,7 +102,9 @@ uint32_t magic_half(uint32_t d) {   // ceil(2^32 / (2 d)) for d >= 1
 bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
     if (a.impl == FA_IMPL_HIP) return false;
     if (bm.mask || a.is_causal || a.p_dropout > 0.f || a.rot_cos) return false;
-    if (a.head_dim <= 32 || a.head_dim > 64) return false;
+    // D = 64 tile: head_dim in (32, 64] (zero-padded); D = 128 tile: head_dim == 128 only (its Q loads
+    // and O stores address whole rows from one base)
+    if (!((a.head_dim > 32 && a.head_dim <= 64) || a.head_dim == 128)) return false;
     if (a.max_seqlen_q <= 0) return false;
     // byte strides must fit the kernel's 32-bit row strides; the magic divisions are exact for
     // n * d <= 2^30 (n < workgroups, d = q-blocks per head or heads)
@@ -111,7 +122,7 @@ bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
 
 hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
     hipFunction_t fn = nullptr;
-    hipError_t e = get_function(a.dtype, &fn);
+    hipError_t e = get_function(a.dtype, a.head_dim > 64 ? 128 : 64, &fn);
     if (e != hipSuccess) return e;
     FaAsmFwdArgs k;
     std::memset(&k, 0, sizeof(k));

@@ -24,12 +24,16 @@ from oracle.attention_ref import attention_ref  # noqa: E402
 _TXT = {}
 
 
-def _kernel(dtype):
-    if dtype not in _TXT:
-        g = gen_fwd.Gen(dtype)
-        blocks, _ = gen_fwd.build(g)
-        _TXT[dtype] = gen_fwd.emit(g, blocks)
-    return _TXT[dtype]
+def _kernel(dtype, hd=64):
+    if (dtype, hd) not in _TXT:
+        gen_fwd.configure(hd)
+        try:
+            g = gen_fwd.Gen(dtype)
+            blocks, _ = gen_fwd.build(g)
+            _TXT[(dtype, hd)] = gen_fwd.emit(g, blocks)
+        finally:
+            gen_fwd.configure(64)
+    return _TXT[(dtype, hd)]
 
 
 def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0):
@@ -56,7 +60,7 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0):
                        H * D * 2, H * D * 2, H * D * 2, H * D * 2, H, lse_stride * 4, c, np.float32(8.0 / c),
                        nqb, nqb * H * B, mg(nqb), mg(H), D, 0)
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
-    asm_sim.Sim(_kernel(dtype), dtype).run((nqb, H, B), pa, mem)
+    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64), dtype).run((nqb, H, B), pa, mem)
     o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
     lse = mem.get(pl).view(np.float32).reshape(B, H, lse_stride)
     to = lambda x: torch.from_numpy(asm_sim.from16(x.astype(np.uint32), dtype))
@@ -97,6 +101,16 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0):
 ])
 def test_asm_forward_in_simulator(lens_q, lens_k, H, D, dtype):
     _run(lens_q, lens_k, H, D, dtype)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("lens_q,lens_k", [
+    ([130], [200]),                   # 3 full tiles + a masked one
+    ([70, 33], [700, 0]),             # 11 tiles (every loop position, last-tile exit); empty key set
+])
+def test_asm_forward_d128_in_simulator(lens_q, lens_k, dtype):
+    """The head_dim = 128 kernel (single-buffered K / V^T fragments, Q and row sums in VGPRs)."""
+    _run(lens_q, lens_k, 1, 128, dtype)
 
 
 def test_asm_forward_rescale_path_in_simulator():

@@ -25,6 +25,7 @@ CFGS = {
     "D32": (8, 12, 2048, 2048, 32, "bf16", False, 0.0, False),
     "D64": (8, 12, 2048, 2048, 64, "bf16", False, 0.0, False),
     "D128": (8, 12, 2048, 2048, 128, "bf16", False, 0.0, False),
+    "D128b16": (16, 12, 4096, 4096, 128, "bf16", False, 0.0, False),   # C4's shape, non-causal
     "C2": (8, 12, 512, 512, 64, "fp16", False, 0.0, False),
     "C3": (8, 12, 2048, 2048, 64, "bf16", True, 0.1, False),
     "C3nd": (8, 12, 2048, 2048, 64, "bf16", True, 0.0, False),    # C3 without dropout (its cost)
@@ -39,6 +40,7 @@ def main():
     ap.add_argument("--mode", required=True, choices=["fwd", "bwd"])
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--warm", type=float, default=0.3)
+    ap.add_argument("--impl", default="auto", choices=["auto", "hip"], help="forward kernel family (FaFwdArgs.impl)")
     a = ap.parse_args()
     B, H, Sq, Sk, D, dts, causal, p, kvpacked = CFGS[a.cfg]
     dt = torch.float16 if dts == "fp16" else torch.bfloat16
@@ -57,7 +59,8 @@ def main():
     rng = hip.reserve_rng(dev) if p > 0 else None
 
     def fwd():
-        return hip.fwd(q, k, v, cu_q, cu_k, Sq, Sk, p, scale, False, causal, False, None, rng_state=rng)
+        return hip.fwd(q, k, v, cu_q, cu_k, Sq, Sk, p, scale, False, causal, False, None, rng_state=rng,
+                       impl=hip.FA_IMPL_HIP if a.impl == "hip" else hip.FA_IMPL_AUTO)
 
     if a.mode == "fwd":
         step = fwd
@@ -91,7 +94,7 @@ def main():
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) * 1e3 / a.launches
-    print(json.dumps({"cfg": a.cfg, "mode": a.mode, "launches": a.launches, "warmup_calls": n_warm,
+    print(json.dumps({"cfg": a.cfg, "mode": a.mode, "impl": a.impl, "launches": a.launches, "warmup_calls": n_warm,
                       "warmup_s": round(time.perf_counter() - t0 - s.elapsed_time(e) / 1e3, 3),
                       "event_us_per_call": round(us, 2)}), flush=True)
 
