@@ -96,14 +96,15 @@ V_TMP = {'A': 116, 'B': 124}    # 8 each
 V_BPA = 132            # ds_bpermute address: alpha of query (l&15)+16(l>>5)  (sum-MFMA lane map)
 V_BPL = 133            # ds_bpermute address: row sum of query l&31
 V_NEGINF = 134
-V_NVREL = 135          # last tile: valid keys of the tile minus 4*hi
+V_NVREL = {'A': 135, 'B': 164}  # masked tiles: keys of the tile the lane's row may see, minus 4*hi
+V_ROW1 = {'A': 165, 'B': 166}   # min(seqlen_k, row + 1 if causal) - 4*hi (per block)
 V_OOFF = {'A': 136, 'B': 140}   # 4 each: O store offsets (dt, g)
 V_LOFF = {'A': 144, 'B': 145}   # LSE store offset
 V_ONEF = 146           # 1.0f
 V_LANE = 147
 V_ETMP = 148           # 16: rotating exp temporaries of the speculative softmax (S stays intact)
-V_MCB = {'A': 164, 'B': 168}    # 4 each (MC_BANKS): copies of m*c in VGPR banks 0..3
-NVGPR = 164
+V_MCB = {'A': 168, 'B': 172}    # 4 each (MC_BANKS): copies of m*c in VGPR banks 0..3
+NVGPR = 168
 # ---- AGPRs
 A_O = {'A': 0, 'B': 32}         # O^T accumulators (2 d-blocks x 16)
 A_L = {'A': 64, 'B': 68}        # row-sum accumulators (16x16 MFMA C)
@@ -130,10 +131,10 @@ def configure(hd):
     """Head-dim tile. 64: the layout above (head_dim in (32, 64]). 128 (head_dim == 128): twice the
     k-steps and d-blocks, single K / V^T fragment buffers (the K reads of tile j+1 follow the last
     QK_B(j) MFMA, the V^T reads of tile j follow PV_B(j-1), one phase earlier), Q / O offsets as
-    one base + immediates, 128 KiB of LDS ring. 248 VGPRs (Q, row sums, indicator among them) + 256
+    one base + immediates, 128 KiB of LDS ring. 252 VGPRs (Q, row sums, indicator among them) + 256
     AGPRs (O, K and V^T fragments)."""
     global D, NKS, NDT, NP, ROWB, KFB, NBK, NBV, TILE, VREG, LDS_BYTES, O_BASE, VREADS_P1, QL_VGPR
-    global V_KADDR, V_VADDR, V_DMA, V_S, V_P, V_MTHR, V_MC, V_TMP, V_BPA, V_BPL, V_NEGINF, V_NVREL
+    global V_KADDR, V_VADDR, V_DMA, V_S, V_P, V_MTHR, V_MC, V_TMP, V_BPA, V_BPL, V_NEGINF, V_NVREL, V_ROW1
     global V_OOFF, V_LOFF, V_ONEF, V_LANE, V_ETMP, V_MCB, NVGPR, A_O, A_L, A_ONES, A_Q, A_KF, A_VF, NAGPR
     assert hd in (64, 128)
     globals().update(_D64)   # the D = 64 layout, then the D = 128 changes
@@ -149,13 +150,14 @@ def configure(hd):
     V_S, V_P = {'A': 4, 'B': 36}, {'A': 68, 'B': 84}
     V_KADDR, V_VADDR, V_DMA = 100, 108, 116
     V_MTHR, V_MC, V_TMP = {'A': 124, 'B': 125}, {'A': 126, 'B': 127}, {'A': 128, 'B': 136}
-    V_BPA, V_BPL, V_NEGINF, V_NVREL = 144, 145, 146, 147
+    V_BPA, V_BPL, V_NEGINF = 144, 145, 146
+    V_NVREL, V_ROW1 = {'A': 147, 'B': 248}, {'A': 249, 'B': 250}
     V_OOFF, V_LOFF = {'A': 148, 'B': 149}, {'A': 150, 'B': 151}
     V_ONEF, V_LANE, V_ETMP = 152, 153, 154
     # VGPRs: Q fragments, row sums and the indicator after the exp temporaries (A_* names kept)
     A_Q, A_L, A_ONES = {'A': 172, 'B': 204}, {'A': 236, 'B': 240}, 244
-    V_MCB = {'A': 248, 'B': 252}
-    NVGPR = 248
+    V_MCB = None           # no room for MC_BANKS copies at D = 128
+    NVGPR = 252
     A_O, A_KF, A_VF = {'A': 0, 'B': 64}, 128, 192
     NAGPR = 256
 
@@ -163,7 +165,7 @@ def configure(hd):
 _D64 = {k: (dict(v) if isinstance(v, dict) else v) for k, v in globals().items()
         if k in ('D', 'NKS', 'NDT', 'NP', 'ROWB', 'KFB', 'NBK', 'NBV', 'TILE', 'VREG', 'LDS_BYTES', 'O_BASE',
                  'VREADS_P1', 'QL_VGPR', 'V_KADDR', 'V_VADDR', 'V_DMA', 'V_S', 'V_P', 'V_MTHR', 'V_MC', 'V_TMP',
-                 'V_BPA', 'V_BPL', 'V_NEGINF', 'V_NVREL', 'V_OOFF', 'V_LOFF', 'V_ONEF', 'V_LANE', 'V_ETMP',
+                 'V_BPA', 'V_BPL', 'V_NEGINF', 'V_NVREL', 'V_ROW1', 'V_OOFF', 'V_LOFF', 'V_ONEF', 'V_LANE', 'V_ETMP',
                  'V_MCB', 'NVGPR', 'A_O', 'A_L', 'A_ONES', 'A_Q', 'A_KF', 'A_VF', 'NAGPR')}
 
 
@@ -183,12 +185,14 @@ def epi_regs(X, idx):
 S_KD, S_VD, S_QD, S_OD, S_LD = 8, 12, 16, 20, 24   # buffer descriptors (4 each)
 S_KD1, S_VD1 = 80, 84  # second K / V descriptor sets (odd tiles; prologue temporaries before)
 S_C, S_THR, S_J, S_NT, S_LAST = 28, 29, 30, 31, 32
+S_CAUSAL, S_MAGIC_BH = 33, 34   # kernel arguments: causal flag, ceil(2^32 / (2 nbh))
+S_MSTART = 39          # first tile of the masked loop (causal: the diagonal band; else the last tile)
 S_KSTEP, S_VSTEP, S_WAVE = 35, 36, 37
 S_M0B = 38             # 1024 * wave: this wave's DMA pieces start at piece `wave`
 S_ARG = 40             # kernel arguments s[40:75]
 S_CU = 76              # cu_seqlens values s[76:79]
 S_T = 80               # temporaries s[80:97]
-NSGPR = 98
+NSGPR = 102
 
 
 class Inst:
@@ -447,7 +451,7 @@ class Gen:
             for i in range(32):
                 st, r = divmod(i, 16)
                 kofs = 32 * st + (r & 3) + 8 * (r >> 2)
-                out.append(V(f'v_cmp_lt_i32 vcc, {kofs}, v{V_NVREL}', 'vcc', [V_NVREL]))
+                out.append(V(f'v_cmp_lt_i32 vcc, {kofs}, v{V_NVREL[X]}', 'vcc', [V_NVREL[X]]))
                 out.append(Inst(f'v_cndmask_b32 v{S + i}, v{V_NEGINF}, v{S + i}, vcc', 'valu', 4,
                                 rd=[f'v{V_NEGINF}', f'v{S + i}', 'vcc'], wr=[f'v{S + i}']))
         if ORDET:
@@ -487,7 +491,7 @@ class Gen:
             for i in range(32):
                 st, r = divmod(i, 16)
                 kofs = 32 * st + (r & 3) + 8 * (r >> 2)
-                out.append(V(f'v_cmp_lt_i32 vcc, {kofs}, v{V_NVREL}', 'vcc', [V_NVREL]))
+                out.append(V(f'v_cmp_lt_i32 vcc, {kofs}, v{V_NVREL[X]}', 'vcc', [V_NVREL[X]]))
                 out.append(Inst(f'v_cndmask_b32 v{S + i}, v{V_NEGINF}, v{S + i}, vcc', 'valu', 4,
                                 rd=[f'v{V_NEGINF}', f'v{S + i}', 'vcc'], wr=[f'v{S + i}']))
         # max tree: 4 chains of v_max3 (ILP 4), then merge, then the lane pair (l, l^32)
@@ -1070,6 +1074,10 @@ def prologue(g):
     p.append(Inst('s_load_dwordx16 s[40:55], s[0:1], 0x0', 'smem', 2, wr=[f's{i}' for i in range(40, 56)]))
     p.append(Inst('s_load_dwordx16 s[56:71], s[0:1], 0x40', 'smem', 2, wr=[f's{i}' for i in range(56, 72)]))
     p.append(Inst('s_load_dwordx4 s[72:75], s[0:1], 0x80', 'smem', 2, wr=[f's{i}' for i in range(72, 76)]))
+    p.append(Inst(f's_load_dword s{S_CAUSAL}, s[0:1], 0x90', 'smem', 2, wr=[f's{S_CAUSAL}']))
+    p.append(Inst(f's_load_dword s{S_MAGIC_BH}, s[0:1], 0x94', 'smem', 2, wr=[f's{S_MAGIC_BH}']))
+    # causal XCD groups: s98 per = G nqb (0: global order), s99 magic(per), s100 G, s101 magic(G)
+    p.append(Inst('s_load_dwordx4 s[98:101], s[0:1], 0x98', 'smem', 2, wr=[f's{i}' for i in range(98, 102)]))
     p.append(raw('s_waitcnt lgkmcnt(0)'))
     if WAVE_MODE == 'early':
         p += wave_id_insts()
@@ -1081,6 +1089,24 @@ def prologue(g):
           S('s_lshr_b32 s85, s80, 3'), S('s_add_u32 s84, s84, s85'),
           S('s_lshl_b32 s85, s84, 1'), S('s_mul_hi_u32 s86, s85, s72'),
           S('s_mul_i32 s87, s86, s70'), S('s_sub_u32 s87, s84, s87'),
+          # causal: global heaviest-first order, rank = L / nbh (s75 = nbh), bh = L - rank nbh,
+          # qb = nqb - 1 - rank (the last q-blocks see the most keys)
+          S('s_lshl_b32 s85, s80, 1'), S(f's_mul_hi_u32 s81, s85, s{S_MAGIC_BH}'),
+          S('s_mul_i32 s82, s81, s75'), S('s_sub_u32 s82, s80, s82'),
+          S('s_sub_u32 s83, s70, 1'), S('s_sub_u32 s83, s83, s81'),
+          # ... or, when the host gave a group size (s98 = per = G nqb > 0), XCD groups as the HIP
+          # kernels (fa_common.h xcd_grouped with full groups): i = L >> 3 on XCD x = L & 7, grp =
+          # i / per, w = i % per, rank = w / G, bh = x (nbh / 8) + grp G + w % G
+          S('s_lshr_b32 s90, s80, 3'), S('s_lshl_b32 s91, s90, 1'), S('s_mul_hi_u32 s91, s91, s99'),
+          S('s_mul_i32 s92, s91, s98'), S('s_sub_u32 s92, s90, s92'),
+          S('s_lshl_b32 s93, s92, 1'), S('s_mul_hi_u32 s93, s93, s101'),
+          S('s_mul_i32 s94, s93, s100'), S('s_sub_u32 s94, s92, s94'),
+          S('s_mul_i32 s95, s91, s100'), S('s_add_u32 s94, s94, s95'),
+          S('s_lshr_b32 s95, s75, 3'), S('s_and_b32 s90, s80, 7'), S('s_mul_i32 s95, s95, s90'),
+          S('s_add_u32 s94, s94, s95'),
+          S('s_sub_u32 s95, s70, 1'), S('s_sub_u32 s95, s95, s93'),
+          S('s_cmp_lg_u32 s98, 0'), S('s_cselect_b32 s82, s94, s82'), S('s_cselect_b32 s83, s95, s83'),
+          S(f's_cmp_lg_u32 s{S_CAUSAL}, 0'), S('s_cselect_b32 s86, s82, s86'), S('s_cselect_b32 s87, s83, s87'),
           S('s_lshl_b32 s85, s86, 1'), S('s_mul_hi_u32 s88, s85, s73'),
           S('s_mul_i32 s89, s88, s66'), S('s_sub_u32 s89, s86, s89'),
           S('s_lshl_b32 s90, s88, 2'),
@@ -1104,7 +1130,13 @@ def prologue(g):
           S(f's_lshl_b32 s{S_LD + 2}, s77, 2'), S(f's_mov_b32 s{S_LD + 3}, 0x00020000')]
     p += [S(f's_mov_b32 s{S_C}, s68'), S(f's_mov_b32 s{S_THR}, s69'),
           S(f's_add_u32 s{S_NT}, s79, 63'), S(f's_lshr_b32 s{S_NT}, s{S_NT}, 6'),
+          # causal: the q-block's rows end at 256 (qb + 1), so 4 (qb + 1) tiles at most, and the
+          # diagonal band (masked loop) starts at tile 4 qb
+          S('s_add_u32 s96, s87, 1'), S('s_lshl_b32 s96, s96, 2'), S(f's_min_u32 s97, s{S_NT}, s96'),
+          S(f's_cmp_lg_u32 s{S_CAUSAL}, 0'), S(f's_cselect_b32 s{S_NT}, s97, s{S_NT}'),
           S(f's_sub_u32 s{S_LAST}, s{S_NT}, 1'), S(f's_mov_b32 s{S_J}, 0'),
+          S('s_lshl_b32 s96, s87, 2'), S(f's_min_u32 s97, s96, s{S_LAST}'),
+          S(f's_cmp_lg_u32 s{S_CAUSAL}, 0'), S(f's_cselect_b32 s{S_MSTART}, s97, s{S_LAST}'),
           S(f's_lshl_b32 s{S_KSTEP}, s63, 7'), S(f's_lshl_b32 s{S_VSTEP}, s64, 7'),
           S(f's_lshl_b32 s{S_M0B}, s{S_WAVE}, 10')]
     # second descriptor sets (odd tiles): one tile (64 rows) further, num_records saturating
@@ -1161,6 +1193,13 @@ def prologue(g):
         p += [V('v_add_u32 v39, s93, v16', 39, [16])]
         if xo:
             p += [V(f'v_add_u32 v39, {xo}, v39', 39, [39])]
+        # keys this lane's row may see: min(seqlen_k, row + 1 if causal), minus 4 hi (the mask
+        # compares register key offsets without the 4 hi of their lane half)
+        p += [V('v_add_u32 v40, 1, v39', 40, [39]),
+              V(f'v_cmp_ne_u32 vcc, s{S_CAUSAL}, v32', 'vcc', [32]),
+              Inst('v_cndmask_b32 v40, v31, v40, vcc', 'valu', rd=['v31', 'v40', 'vcc'], wr=['v40']),
+              V('v_min_u32 v40, s79, v40', 40, [40]), V('v_lshlrev_b32 v41, 2, v17', 41, [17]),
+              V(f'v_sub_u32 v{V_ROW1[X]}, v40, v41', V_ROW1[X], [40, 41])]
         if O_BASE:
             p += [V('v_mul_lo_u32 v42, v39, s62', 42, [39]),
                   V(f'v_lshl_add_u32 v{qoff[X]}, v17, 4, v42', qoff[X], [17, 42]),
@@ -1263,16 +1302,29 @@ def dump_block(regs):
 DUMP = None   # (point, [registers]) set by --dump
 
 
+def nvrel_insts():
+    """Per-block key limits of a masked tile: NVREL_X = ROW1_X - 64 j."""
+    return [S(f's_lshl_b32 s96, s{S_J}, 6')] + \
+           [V(f'v_subrev_u32 v{V_NVREL[X]}, s96, v{V_ROW1[X]}', V_NVREL[X], [V_ROW1[X]]) for X in 'AB']
+
+
+def masked_tile(g, t, rescue):
+    """Loop position t of the masked loop: tiles from S_MSTART (the causal diagonal band) up to
+    the last one, which exits to .Llast{t}."""
+    blk = [label(f'.Lmask{t}'), S(f's_cmp_eq_u32 s{S_J}, s{S_LAST}'), raw(f's_cbranch_scc1 .Llast{t}')]
+    blk += nvrel_insts()
+    blk += g.phase1(t, masked=True, rescue=rescue)
+    blk += g.phase2(t, masked=True, rescue=rescue)
+    blk += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier'), S(f's_add_u32 s{S_J}, s{S_J}, 1')]
+    if t == U - 1:
+        blk.append(raw('s_branch .Lmask0'))
+    return blk
+
+
 def last_tile(g, t, rescue):
     """Tile t = nt - 1 (position t of the unrolled loop): masked softmax of both blocks, no
     next-tile reads or DMA, then P.V of block B and the two epilogues."""
-    b = [label(f'.Llast{t}')]
-    tmp = V_TMP['A'] + 7
-    b += [S(f's_lshl_b32 s96, s{S_J}, 6'), S('s_sub_u32 s96, s79, s96'),
-          V(f'v_mov_b32 v{V_NVREL}, s96', V_NVREL, []),
-          V(f'v_bfe_u32 v{tmp}, v{V_LANE}, 5, 1', tmp, [V_LANE]),
-          V(f'v_lshlrev_b32 v{tmp}, 2, v{tmp}', tmp, [tmp]),
-          V(f'v_sub_u32 v{V_NVREL}, v{V_NVREL}, v{tmp}', V_NVREL, [V_NVREL, tmp])]
+    b = [label(f'.Llast{t}')] + nvrel_insts()
     b += g.phase1(t, masked=True, last=True, rescue=rescue)
     b += g.phase2(t, masked=True, last=True, rescue=rescue)
     b += [mark()] + place(g.pv_sum('B', t)[0], g.epilogue('A'))
@@ -1292,7 +1344,7 @@ def build(g):
         if t == 0:
             blk.append(raw('.p2align 6'))
             blk.append(label('.Lloop'))
-        blk += [S(f's_cmp_eq_u32 s{S_J}, s{S_LAST}'), raw(f's_cbranch_scc1 .Llast{t}')]
+        blk += [S(f's_cmp_ge_u32 s{S_J}, s{S_MSTART}'), raw(f's_cbranch_scc1 .Lmask{t}')]
         blk += g.phase1(t, rescue=rescue)
         if DUMP and DUMP[0] == 'p1' and t == 0:
             blk += dump_block(DUMP[1])
@@ -1305,21 +1357,26 @@ def build(g):
         if t == U - 1:
             blk.append(raw('s_branch .Lloop'))
         tiles.append(blk)
+    masks = [masked_tile(g, t, rescue) for t in range(U)]
     lasts = [last_tile(g, t, rescue) for t in range(U)]
     empty = [label('.Lempty'), mark()] + g.epilogue('A') + [mark()] + g.epilogue('B') + \
             [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
     end = [label('.Lend'), raw('s_endpgm')]
     # control-flow paths for the hazard pass
     paths = []
-    paths.append(lambda: refs(pro) + sum((refs(b) for b in tiles), []) + sum((refs(b) for b in tiles), []))
+    def seq(blks):
+        return sum((refs(b) for b in blks), [])
+    paths.append(lambda: refs(pro) + seq(tiles) + seq(tiles))
     for t in range(U):
-        paths.append(lambda t=t: refs(pro) + sum((refs(b) for b in tiles), []) + sum((refs(b) for b in tiles[:t]), [])
-                     + refs(lasts[t]))
+        # main loop -> masked loop entered at position t -> a full masked round
+        paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
+        # masked loop -> last tile at position t
+        paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(masks) + seq(masks[:t]) + refs(lasts[t]))
     paths.append(lambda: refs(pro) + refs(empty))
     # rescale blocks entered from their branch: the 40 instructions before it, the block, the rest
     def resc_path(rb):
         ret = rb[-1].txt.split()[-1]
-        for blk in tiles + lasts:
+        for blk in tiles + masks + lasts:
             for i, x in enumerate(blk):
                 if x.kind == 'br' and x.txt.endswith(f'{ret}:'):
                     lo = max(0, i - 40)
@@ -1328,7 +1385,7 @@ def build(g):
     for rb in rescue:
         paths.append(lambda rb=rb: resc_path(rb))
     n = fix_paths(paths)
-    blocks = [pro] + tiles + lasts + [empty, end] + rescue
+    blocks = [pro] + tiles + masks + lasts + [empty, end] + rescue
     return blocks, n
 
 
@@ -1383,7 +1440,7 @@ def emit(g, blocks):
     return '\n'.join(lines)
 
 
-KARG_BYTES = 144
+KARG_BYTES = 168
 
 
 def expand_regs(spec):

@@ -6,7 +6,7 @@
 // on the caller's stream (so it is captured into hipGraphs like the HIP kernels).
 //
 // It serves the north-star shape class: head_dim in (32, 64] (the D=64 tile) or 128 (the D=128
-// tile), fp16/bf16, non-causal, no dropout, dense (no block mask), no fused rotary. Everything else keeps the HIP
+// tile), fp16/bf16, causal or not, no dropout, dense (no block mask), no fused rotary. Everything else keeps the HIP
 // kernels of fa_fwd_kernel.h. Semantics are the same: var-len sequences through cu_seqlens,
 // rows past a sequence neither read nor written, LSE = m*scale + ln(sum) (-inf for no keys).
 #include <hip/hip_runtime.h>
@@ -47,11 +47,17 @@ struct FaAsmFwdArgs {
     uint32_t magic_nqb;                    // ceil(2^32 / (2 nqb)): Lp / nqb = mulhi(2 Lp, magic)
     uint32_t magic_h;                      // ceil(2^32 / (2 H))
     uint32_t head_dim;
-    uint32_t pad;
+    uint32_t nbh;                          // batch * heads
+    uint32_t causal;                       // top-left causal mask (col <= row), heaviest q-blocks first
+    uint32_t magic_nbh;                    // ceil(2^32 / (2 nbh))
+    // causal XCD groups (fa_common.h xcd_grouped): each XCD runs its nbh / 8 heads in groups of G,
+    // heaviest q-block first across a group; per = G nqb (0: the global heaviest-first order)
+    uint32_t per, magic_per, group, magic_group;
 };
-static_assert(sizeof(FaAsmFwdArgs) == 144, "FaAsmFwdArgs layout (gen_fwd.py KARG_BYTES)");
+static_assert(sizeof(FaAsmFwdArgs) == 168, "FaAsmFwdArgs layout (gen_fwd.py KARG_BYTES)");
 static_assert(offsetof(FaAsmFwdArgs, q_rs) == 88 && offsetof(FaAsmFwdArgs, c) == 112 &&
-              offsetof(FaAsmFwdArgs, magic_nqb) == 128 && offsetof(FaAsmFwdArgs, head_dim) == 136,
+              offsetof(FaAsmFwdArgs, magic_nqb) == 128 && offsetof(FaAsmFwdArgs, head_dim) == 136 &&
+                  offsetof(FaAsmFwdArgs, causal) == 144,
               "FaAsmFwdArgs offsets (gen_fwd.py prologue)");
 
 namespace {
@@ -101,7 +107,7 @@ uint32_t magic_half(uint32_t d) {   // ceil(2^32 / (2 d)) for d >= 1
 
 bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
     if (a.impl == FA_IMPL_HIP) return false;
-    if (bm.mask || a.is_causal || a.p_dropout > 0.f || a.rot_cos) return false;
+    if (bm.mask || a.p_dropout > 0.f || a.rot_cos) return false;
     // D = 64 tile: head_dim in (32, 64] (zero-padded); D = 128 tile: head_dim == 128 only (its Q loads
     // and O stores address whole rows from one base)
     if (!((a.head_dim > 32 && a.head_dim <= 64) || a.head_dim == 128)) return false;
@@ -114,7 +120,9 @@ bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
         return false;
     const int64_t nqb = (a.max_seqlen_q + kRows - 1) / kRows;
     const int64_t nwg = nqb * a.nheads * a.batch;
-    const int64_t dmax = nqb > a.nheads ? nqb : a.nheads;
+    const int64_t nbh = (int64_t)a.nheads * a.batch;
+    int64_t dmax = nqb > a.nheads ? nqb : a.nheads;
+    if (nbh > dmax) dmax = nbh;
     if (nwg >= ((int64_t)1 << 30) / dmax) return false;
     if (nqb > 65535 || a.nheads > 65535 || a.batch > 65535) return false;
     return true;
@@ -151,6 +159,21 @@ hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
     k.magic_nqb = magic_half(nqb);
     k.magic_h = magic_half((uint32_t)a.nheads);
     k.head_dim = (uint32_t)a.head_dim;
+    k.nbh = (uint32_t)a.nheads * (uint32_t)a.batch;
+    k.causal = a.is_causal ? 1u : 0u;
+    k.magic_nbh = magic_half(k.nbh);
+    if (a.is_causal && k.nbh % 8 == 0) {
+        // G nqb ~ 2x the workgroups one XCD runs at once (one per CU: 32), G dividing the XCD's
+        // nbh / 8 heads so that every group is full (the HIP kernels' measured choice, x2 slots)
+        const uint32_t nh = k.nbh / 8, want = (64 + nqb - 1) / nqb;
+        uint32_t g = 1;
+        for (uint32_t c = 1; c <= nh && c <= want; ++c)
+            if (nh % c == 0) g = c;
+        k.per = g * nqb;
+        k.magic_per = magic_half(k.per);
+        k.group = g;
+        k.magic_group = magic_half(g);
+    }
     size_t size = sizeof(k);
     void *config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
     e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, kRows, 1, 1, 0, stream, nullptr, config);

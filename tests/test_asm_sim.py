@@ -36,7 +36,7 @@ def _kernel(dtype, hd=64):
     return _TXT[(dtype, hd)]
 
 
-def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0):
+def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False):
     rng = np.random.default_rng(seed)
     cv = asm_sim.bf16_bits if dtype == "bf16" else asm_sim.f16_bits
     B, tq, tk = len(lens_q), sum(lens_q), sum(lens_k)
@@ -56,9 +56,15 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0):
     c = np.float32(scale * 1.4426950408889634)
     nqb = (maxq + 255) // 256
     mg = lambda d: ((1 << 32) + 2 * d - 1) // (2 * d)
-    karg = struct.pack("<7Q4Q4I2I2f2I2I2I", pq, pk, pv, po, pl, pcq, pck, D * 2, D * 2, D * 2, D * 2,
+    per = grp = 0
+    if causal and (H * B) % 8 == 0:     # fa_asm.cpp's group choice
+        nh, want = H * B // 8, (64 + nqb - 1) // nqb
+        grp = max(c for c in range(1, min(nh, want) + 1) if nh % c == 0)
+        per = grp * nqb
+    karg = struct.pack("<7Q4Q4I2I2f2I2I2I2I4I", pq, pk, pv, po, pl, pcq, pck, D * 2, D * 2, D * 2, D * 2,
                        H * D * 2, H * D * 2, H * D * 2, H * D * 2, H, lse_stride * 4, c, np.float32(8.0 / c),
-                       nqb, nqb * H * B, mg(nqb), mg(H), D, 0)
+                       nqb, nqb * H * B, mg(nqb), mg(H), D, H * B, int(causal), mg(H * B),
+                       per, mg(per) if per else 0, grp, mg(grp) if grp else 0)
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
     asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64), dtype).run((nqb, H, B), pa, mem)
     o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
@@ -76,16 +82,21 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0):
         # the reference's own oracle at fp32 and at the input precision (the 2x rule of
         # tests/test_flash_attn.py:407-409)
         args = (qf[sq][None], kf[sk][None], vf[sk][None])
-        ref = attention_ref(*args, upcast=True)[0][0] if scale == D ** -0.5 else None
+        ref = attention_ref(*args, upcast=True, causal=causal)[0][0] if scale == D ** -0.5 else None
+        cmask = torch.triu(torch.ones(lens_q[b], lens_k[b], dtype=torch.bool), 1) if causal else None
         if ref is None:
             s = torch.einsum("qhd,khd->hqk", qf[sq].double(), kf[sk].double()) * scale
+            if causal:
+                s = s.masked_fill(cmask, float("-inf"))
             ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), vf[sk].double()).float()
             base = 4e-3
         else:
-            lo = attention_ref(*(x.to(tdt) for x in args), upcast=False)[0][0].float()
+            lo = attention_ref(*(x.to(tdt) for x in args), upcast=False, causal=causal)[0][0].float()
             base = (lo - ref).abs().max().item()
         assert (o_b - ref).abs().max().item() <= 2 * base + 1e-4, (b, (o_b - ref).abs().max().item(), base)
         s = torch.einsum("qhd,khd->hqk", qf[sq].double(), kf[sk].double()) * scale
+        if causal:
+            s = s.masked_fill(cmask, float("-inf"))
         ref_lse = torch.logsumexp(s, -1).numpy()
         # the row sums cover the 16-bit-rounded P (what multiplies V): up to 2^-8 relative in the
         # sum, so the LSE is within 4e-3
@@ -111,6 +122,21 @@ def test_asm_forward_in_simulator(lens_q, lens_k, H, D, dtype):
 def test_asm_forward_d128_in_simulator(lens_q, lens_k, dtype):
     """The head_dim = 128 kernel (single-buffered K / V^T fragments, Q and row sums in VGPRs)."""
     _run(lens_q, lens_k, 1, 128, dtype)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("lens_q,lens_k", [
+    ([300], [300]),                   # two q-blocks: the diagonal band (masked loop) of each, LPT order
+    ([70, 600], [130, 520]),          # var-len, Sq != Sk (top-left aligned), unequal band positions
+])
+def test_asm_forward_causal_in_simulator(lens_q, lens_k, D):
+    _run(lens_q, lens_k, 1, D, "bf16", causal=True)
+
+
+def test_asm_forward_causal_xcd_groups_in_simulator():
+    """8 (batch, head) pairs: the XCD-grouped causal order (every workgroup still covers its own
+    q-block exactly once)."""
+    _run([300] * 4, [300] * 4, 2, 64, "bf16", causal=True)
 
 
 def test_asm_forward_rescale_path_in_simulator():

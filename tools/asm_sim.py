@@ -268,7 +268,7 @@ class Sim:
                 w.pc = self.labels[a[0]]
             return
         if op.startswith('s_load_dword'):
-            n = {'s_load_dwordx2': 2, 's_load_dwordx4': 4, 's_load_dwordx16': 16}[op]
+            n = {'s_load_dword': 1, 's_load_dwordx2': 2, 's_load_dwordx4': 4, 's_load_dwordx16': 16}[op]
             f, i, cnt = self.regs(w, a[0])
             _, b, _ = self.regs(w, a[1])
             addr = (int(w.s[b]) | (int(w.s[b + 1]) << 32)) + int(a[2], 0)
@@ -336,6 +336,9 @@ class Sim:
             return
         elif op == 's_cmp_eq_u32':
             w.scc = self.sread(w, a[0]) == x
+            return
+        elif op == 's_cmp_lg_u32':
+            w.scc = self.sread(w, a[0]) != x
             return
         else:
             raise NotImplementedError(op)
@@ -410,6 +413,10 @@ class Sim:
                 r = (src[0].astype(np.uint64) + src[1]).astype(np.uint64) & 0xFFFFFFFF
             elif op == 'v_sub_u32':
                 r = (src[0].astype(np.int64) - src[1].astype(np.int64)) & 0xFFFFFFFF
+            elif op == 'v_subrev_u32':
+                r = (src[1].astype(np.int64) - src[0].astype(np.int64)) & 0xFFFFFFFF
+            elif op == 'v_min_u32':
+                r = np.minimum(src[0], src[1])
             elif op == 'v_lshl_add_u32':
                 r = ((src[0].astype(np.uint64) << src[1].astype(np.uint64)) + src[2]) & 0xFFFFFFFF
             elif op == 'v_lshl_or_b32':
