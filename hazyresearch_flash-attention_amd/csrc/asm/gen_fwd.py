@@ -1077,7 +1077,8 @@ def prologue(g):
     p.append(Inst(f's_load_dword s{S_CAUSAL}, s[0:1], 0x90', 'smem', 2, wr=[f's{S_CAUSAL}']))
     p.append(Inst(f's_load_dword s{S_MAGIC_BH}, s[0:1], 0x94', 'smem', 2, wr=[f's{S_MAGIC_BH}']))
     # causal XCD groups: s98 per = G nqb (0: global order), s99 magic(per), s100 G, s101 magic(G)
-    p.append(Inst('s_load_dwordx4 s[98:101], s[0:1], 0x98', 'smem', 2, wr=[f's{i}' for i in range(98, 102)]))
+    p.append(Inst('s_load_dwordx2 s[98:99], s[0:1], 0x98', 'smem', 2, wr=['s98', 's99']))
+    p.append(Inst('s_load_dwordx2 s[100:101], s[0:1], 0xa0', 'smem', 2, wr=['s100', 's101']))
     p.append(raw('s_waitcnt lgkmcnt(0)'))
     if WAVE_MODE == 'early':
         p += wave_id_insts()
@@ -1261,6 +1262,7 @@ def prologue(g):
     p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
     p += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier')]
+    p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
     # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
     p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
     p += [raw('s_nop 7'), raw('s_nop 3')]
@@ -1301,6 +1303,44 @@ def dump_block(regs):
 
 DUMP = None   # (point, [registers]) set by --dump
 
+# 'stamps' probe (tools/asm_wg_timeline.py, D = 64 only): s_memrealtime (100 MHz) at kernel entry
+# (v168:169), after the prologue's first barrier (v180:181), at the last tile's entry (v170:171)
+# and after the final store drain (v172:173); HW_ID / XCC_ID, the workgroup ids s2..s4 and the
+# wave index; lane 0 claims a 64-byte record with a vector atomic on the counter at the pointer
+# in the 8 kernel-argument bytes after KARG_BYTES and writes the record with vector stores.
+STAMP_V = 168
+
+
+def stamp(lo):
+    return [raw('s_memrealtime s[96:97]'), raw('s_waitcnt lgkmcnt(0)'),
+            raw(f'v_mov_b32 v{lo}, s96'), raw(f'v_mov_b32 v{lo + 1}, s97')]
+
+
+def stamp_entry():
+    if 'stamps' not in PROBE:
+        return []
+    b = STAMP_V
+    return stamp(b) + [raw('s_getreg_b32 s96, hwreg(HW_REG_HW_ID)'), raw('s_getreg_b32 s97, hwreg(HW_REG_XCC_ID)'),
+                       raw(f'v_mov_b32 v{b + 6}, s96'), raw(f'v_mov_b32 v{b + 7}, s97'),
+                       raw(f'v_mov_b32 v{b + 8}, s2'), raw(f'v_mov_b32 v{b + 9}, s3'), raw(f'v_mov_b32 v{b + 10}, s4')]
+
+
+def stamp_exit():
+    if 'stamps' not in PROBE:
+        return []
+    b = STAMP_V
+    return stamp(b + 4) + [
+        raw(f's_load_dwordx2 s[98:99], s[0:1], {KARG_BYTES:#x}'), raw('s_waitcnt lgkmcnt(0)'),
+        raw(f'v_mov_b32 v{b + 11}, s{S_WAVE}'), raw('s_mov_b64 exec, 1'),
+        raw(f'v_mov_b32 v{b + 14}, 1'), raw(f'v_mov_b32 v{b + 15}, 0'),
+        raw(f'global_atomic_add v{b + 14}, v{b + 15}, v{b + 14}, s[98:99] sc0'), raw('s_waitcnt vmcnt(0)'),
+        raw(f'v_lshlrev_b32 v{b + 14}, 6, v{b + 14}'), raw(f'v_add_u32 v{b + 14}, 64, v{b + 14}'), raw('s_nop 1'),
+        raw(f'global_store_dwordx4 v{b + 14}, v[{b}:{b + 3}], s[98:99]'),
+        raw(f'global_store_dwordx4 v{b + 14}, v[{b + 4}:{b + 7}], s[98:99] offset:16'),
+        raw(f'global_store_dwordx4 v{b + 14}, v[{b + 8}:{b + 11}], s[98:99] offset:32'),
+        raw(f'global_store_dwordx2 v{b + 14}, v[{b + 12}:{b + 13}], s[98:99] offset:48'),
+        raw('s_waitcnt vmcnt(0)')]
+
 
 def nvrel_insts():
     """Per-block key limits of a masked tile: NVREL_X = ROW1_X - 64 j."""
@@ -1324,18 +1364,18 @@ def masked_tile(g, t, rescue):
 def last_tile(g, t, rescue):
     """Tile t = nt - 1 (position t of the unrolled loop): masked softmax of both blocks, no
     next-tile reads or DMA, then P.V of block B and the two epilogues."""
-    b = [label(f'.Llast{t}')] + nvrel_insts()
+    b = [label(f'.Llast{t}')] + (stamp(STAMP_V + 2) if 'stamps' in PROBE else []) + nvrel_insts()
     b += g.phase1(t, masked=True, last=True, rescue=rescue)
     b += g.phase2(t, masked=True, last=True, rescue=rescue)
     b += [mark()] + place(g.pv_sum('B', t)[0], g.epilogue('A'))
     b += [mark()] + g.epilogue('B')
-    b += [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
+    b += [raw('s_waitcnt vmcnt(0)')] + stamp_exit() + [raw('s_endpgm')]
     return b
 
 
 def build(g):
     rescue = []
-    pro = prologue(g)
+    pro = stamp_entry() + prologue(g)
     if DUMP and DUMP[0] == 'pro':
         pro += dump_block(DUMP[1])
     tiles = []
@@ -1501,6 +1541,11 @@ def main():
         MC_BANKS = bool(args.mcbanks)
     if MC_BANKS:
         NVGPR = max(NVGPR, V_MCB['B'] + 4)
+    global KARG_BYTES
+    if 'stamps' in PROBE:
+        assert args.hd == 64 and NVGPR <= STAMP_V
+        NVGPR = STAMP_V + 16
+        KARG_BYTES += 8
     g = Gen(args.dtype)
     blocks, n = build(g)
     txt = emit(g, blocks)

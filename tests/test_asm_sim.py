@@ -143,3 +143,19 @@ def test_asm_forward_rescale_path_in_simulator():
     """A large softmax scale makes later tiles pass the running max by more than 2^8: the
     out-of-line rescale block (O, row sums and the permuted alpha) runs past tile 0."""
     _run([70], [300], 1, 64, "bf16", scale=3.0)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("hd", [64, 128])
+def test_generated_kernel_assembles(dtype, hd, tmp_path):
+    """The simulator does not check encodings (register alignment, gfx950 operand forms): the
+    product kernels must also assemble for gfx950, as build.py does."""
+    import subprocess
+    llvm = "/opt/rocm/lib/llvm/bin/clang"
+    if not os.path.exists(llvm):
+        pytest.skip("no ROCm LLVM")
+    s = tmp_path / "k.s"
+    s.write_text(_kernel(dtype, hd))
+    r = subprocess.run([llvm, "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c", str(s),
+                        "-o", str(tmp_path / "k.o")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -36,13 +36,18 @@ CFGS = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfg", required=True, choices=sorted(CFGS))
+    ap.add_argument("--cfg", required=True, help="a CFGS name or B,H,Sq,Sk,D[,c] (bf16; c: causal)")
     ap.add_argument("--mode", required=True, choices=["fwd", "bwd"])
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--warm", type=float, default=0.3)
     ap.add_argument("--impl", default="auto", choices=["auto", "hip"], help="forward kernel family (FaFwdArgs.impl)")
     a = ap.parse_args()
-    B, H, Sq, Sk, D, dts, causal, p, kvpacked = CFGS[a.cfg]
+    if a.cfg in CFGS:
+        B, H, Sq, Sk, D, dts, causal, p, kvpacked = CFGS[a.cfg]
+    else:
+        f = a.cfg.split(",")
+        B, H, Sq, Sk, D = map(int, f[:5])
+        dts, causal, p, kvpacked = "bf16", len(f) > 5 and f[5] == "c", 0.0, False
     dt = torch.float16 if dts == "fp16" else torch.bfloat16
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
