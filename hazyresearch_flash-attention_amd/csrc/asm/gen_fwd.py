@@ -116,6 +116,11 @@ NAGPR = 236
 O_BASE = False         # Q loads / O stores from one row base + immediates (requires head_dim == D)
 QL_VGPR = False        # Q fragments, row sums and the 0/1 indicator in VGPRs (D = 128: AGPRs hold
 #                        O, K and V^T fragments, 256, the most an AGPR index reaches)
+NWAVES = 4             # waves per workgroup (8: the two-waves-per-SIMD form, configure(64, 8))
+BLOCKS = 'AB'          # 32-row query blocks of a wave
+NETMP = 16             # rotating exp temporaries
+V_ORT = None           # OR-test accumulator (None: V_TMP[X])
+V_EPT = None           # epilogue temporaries (None: V_TMP[X])
 
 
 def rq(base):
@@ -127,17 +132,50 @@ def rqn(base, n=4):
     return rv(base, n) if QL_VGPR else ra(base, n)
 
 
-def configure(hd):
+def configure(hd, waves=4):
     """Head-dim tile. 64: the layout above (head_dim in (32, 64]). 128 (head_dim == 128): twice the
     k-steps and d-blocks, single K / V^T fragment buffers (the K reads of tile j+1 follow the last
     QK_B(j) MFMA, the V^T reads of tile j follow PV_B(j-1), one phase earlier), Q / O offsets as
     one base + immediates, 128 KiB of LDS ring. 252 VGPRs (Q, row sums, indicator among them) + 256
-    AGPRs (O, K and V^T fragments)."""
+    AGPRs (O, K and V^T fragments).
+
+    waves=8 (D = 64, head_dim == 64): two waves per SIMD, each owning ONE 32-row block in at most
+    256 registers (132 VGPRs + 120 AGPRs). The two register buffers 'A' / 'B' of S and P are then
+    the tiles of even / odd index of that block (O, Q, row sums, m are shared): one phase per tile,
+    QK(t+1) + PV(t-1) + row sums beside the softmax of tile t; single K / V^T fragment buffers;
+    one 1-KiB DMA piece per tensor, tile and wave."""
     global D, NKS, NDT, NP, ROWB, KFB, NBK, NBV, TILE, VREG, LDS_BYTES, O_BASE, VREADS_P1, QL_VGPR
     global V_KADDR, V_VADDR, V_DMA, V_S, V_P, V_MTHR, V_MC, V_TMP, V_BPA, V_BPL, V_NEGINF, V_NVREL, V_ROW1
     global V_OOFF, V_LOFF, V_ONEF, V_LANE, V_ETMP, V_MCB, NVGPR, A_O, A_L, A_ONES, A_Q, A_KF, A_VF, NAGPR
-    assert hd in (64, 128)
-    globals().update(_D64)   # the D = 64 layout, then the D = 128 changes
+    global NWAVES, BLOCKS, NETMP, V_ORT, V_EPT, EXP_LAG, CVT_LAG
+    assert hd in (64, 128) and waves in (4, 8)
+    globals().update(_D64)   # the D = 64 layout, then the D = 128 / 8-wave changes
+    EXP_LAG, CVT_LAG = 4, 4
+    if waves == 8:
+        assert hd == 64
+        NWAVES, BLOCKS, NETMP = 8, 'A', 8
+        EXP_LAG, CVT_LAG = 3, 3
+        NP, NBK, NBV = 1, 1, 1
+        O_BASE, VREADS_P1 = True, False
+        V_KADDR, V_VADDR, V_DMA = 4, 8, 12
+        V_S, V_P = {'A': 16, 'B': 48}, {'A': 80, 'B': 96}
+        V_MTHR = {'A': 112, 'B': 112}
+        V_MC = {'A': 113, 'B': 113}
+        V_ORT = 114
+        V_TMP = dict(V_P)          # rescale temporaries: the P buffer the rescale recomputes anyway
+        V_BPA, V_BPL, V_NEGINF = 115, 116, 117
+        V_NVREL, V_ROW1 = {'A': 118, 'B': 118}, {'A': 119, 'B': 119}
+        V_OOFF, V_LOFF = {'A': 120, 'B': 120}, {'A': 121, 'B': 121}
+        V_ONEF, V_LANE, V_ETMP = 122, 123, 124
+        V_EPT = V_ETMP
+        V_MCB = None
+        NVGPR = 132
+        A_O, A_L, A_ONES = {'A': 0, 'B': 0}, {'A': 32, 'B': 32}, 36
+        A_Q = {'A': 40, 'B': 40}
+        A_KF, A_VF = 56, 88
+        NAGPR = 120
+        return
+    NWAVES, BLOCKS, NETMP, V_ORT, V_EPT = 4, 'AB', 16, None, None
     if hd == 64:
         return
     D, NKS, NDT, NP, ROWB, KFB = hd, hd // 16, hd // 32, hd // 32, 2 * hd, hd // 2
@@ -261,7 +299,7 @@ class Gen:
         self.cvt = 'v_cvt_pk_bf16_f32' if dtype == 'bf16' else 'v_cvt_pk_f16_f32'
         self.one2 = 0x3F803F80 if dtype == 'bf16' else 0x3C003C00
         self.nlabel = 0
-        self.name = f'fa_fwd_d{D}_{dtype}_asm'
+        self.name = f'fa_fwd_d{D}{"w8" if NWAVES == 8 else ""}_{dtype}_asm'
 
     def lab(self, stem):
         self.nlabel += 1
@@ -367,7 +405,7 @@ class Gen:
             out.append(salu(f's_sub_u32 s{desc + 2}, s{desc + 2}, {st}', rd=[dregs[2], st], wr=[dregs[2], 'scc']))
             out.append(salu(f's_cselect_b32 s{desc + 2}, 0, s{desc + 2}', rd=[dregs[2], 'scc'], wr=[dregs[2]]))
         for i in range(NP):
-            m0 = region + (t % R) * TILE + 4096 * i   # + 1024 * wave (S_M0B)
+            m0 = region + (t % R) * TILE + 1024 * NWAVES * i   # + 1024 * wave (S_M0B)
             voff = V_DMA + (0 if kind == 'K' else NP) + i
             out.append(Inst(f's_add_u32 m0, s{S_M0B}, {m0}', 'm0', 2, rd=[f's{S_M0B}'], wr=['m0', 'scc']))
             out.append(Inst(f'buffer_load_dwordx4 v{voff}, s[{desc}:{desc + 3}], 0 offen lds', 'dma', 16,
@@ -390,21 +428,21 @@ class Gen:
         chain behind the cvts, then vcc = lanes holding some P >= 2: bit 14 of either half is
         the top exponent bit of a bf16 / f16 >= 2, and of inf / NaN)."""
         S, P, E = V_S[X], V_P[X], V_ETMP
-        assert EXP_LAG + CVT_LAG + 1 < 16
+        assert EXP_LAG + CVT_LAG + 1 < NETMP
         steps = []
         for i in range(32):
-            e = E + i % 16
+            e = E + i % NETMP
             m = self.mc_reg(X, S + i, mc)
             steps.append((i, 0, Inst(f'v_fma_f32 v{e}, v{S + i}, s{S_C}, -v{m}', 'valu', 4,
                                      rd=[f'v{S + i}', f's{S_C}', f'v{m}'], wr=[f'v{e}'])))
             steps.append((i + EXP_LAG, 1, V(f'v_exp_f32 v{e}, v{e}', e, [e], kind='trans', cost=8)))
         cvt_at = {}
         for q in range(16):
-            a, b = E + (2 * q) % 16, E + (2 * q + 1) % 16
+            a, b = E + (2 * q) % NETMP, E + (2 * q + 1) % NETMP
             cvt_at[q] = 2 * q + 1 + EXP_LAG + CVT_LAG
             steps.append((cvt_at[q], 2, V(f'{self.cvt} v{P + q}, v{a}, v{b}', P + q, [a, b])))
         if ortest:
-            T = V_TMP[X]
+            T = V_TMP[X] if V_ORT is None else V_ORT
             groups = [(0, 1, 2)] + [(2 * k + 1, 2 * k + 2) for k in range(1, 7)] + [(15,)]
             for gi, grp in enumerate(groups):
                 srcs = ([] if gi == 0 else [T]) + [P + q for q in grp]
@@ -463,7 +501,7 @@ class Gen:
             # max ops spread over the first 70 % of the exp stream
             out += merge(ex, [(i, x) for i, x in zip(spread(len(mx), 2, int(len(ex) * 0.7)), mx)])
         resc, ret = self.lab(f'resc{X}'), self.lab(f'ret{X}')
-        touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], D // 2) + rqn(A_L[X]) + rv(V_ETMP, 16) + rv(P, 16)
+        touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], D // 2) + rqn(A_L[X]) + rv(V_ETMP, NETMP) + rv(P, 16)
         if MC_BANKS:
             touched += rv(V_MCB[X], 4)
         out.append(Inst(f's_cbranch_vccnz {resc}\n{ret}:', 'br', 4, rd=['vcc'] + touched, wr=touched))
@@ -637,7 +675,7 @@ class Gen:
     def epilogue(self, X):
         """Normalise O_X by the row sum, store O (16-B stores after a permlane32 pair swap,
         T21) and the LSE = (m c + log2 l) ln 2; an empty row (l == 0) gets 0 and -inf."""
-        S, T, mc = V_S[X], V_TMP[X], V_MC[X]
+        S, T, mc = V_S[X], (V_TMP[X] if V_EPT is None else V_EPT), V_MC[X]
         O, L = A_O[X], A_L[X]
         e = []
         if QL_VGPR:
@@ -724,6 +762,44 @@ class Gen:
         fill = merge(sm, [(i, x) for i, x in zip(spread(len(vr), 1, 56), vr)] +
                      [(i, x) for i, x in zip(spread(len(dma), 30, len(sm) - 10), dma)])
         return [mark()] + place(mf, fill)
+
+    def phase_w8(self, t, masked=False, last=False, rescue=None):
+        """8-wave form, tile t (one 32-row block per wave; 'A'/'B' = register buffers of even/odd
+        tiles): QK(t+1) + PV(t-1) + row sums beside the softmax of tile t. The single K buffer
+        takes K(t+2) behind the QK MFMAs that read K(t+1); the single V^T buffer takes V(t)
+        behind the P.V MFMA that read each fragment of V(t-1). DMA: K(t+1+DIST), V(t+DIST)."""
+        X, Y, Z = par(t), par(t + 1), par(t - 1)
+        qk = [] if last else self.qk(Y, t + 1)
+        pv, use = self.pv_sum(Z, t - 1)
+        mf = qk + pv
+        sm = self.softmax(X, masked, rescue)
+        kr = [] if last else self.kreads(t + 2)
+        for x in kr:
+            x.not_before = len(qk)
+        vr = []
+        for f, ins in self.vreads(t):
+            ins.not_before = len(qk) + use[f] + 1
+            vr.append(ins)
+        dma = [] if last else self.dma('K', t + 1 + DIST) + self.dma('V', t + DIST)
+        # the rescale branch (end of the softmax stream) scales the O and row sums that this
+        # phase's PV(t-1) MFMAs accumulate into: it follows every MFMA of the phase
+        br = sm[-1] if sm and sm[-1].kind == 'br' else None
+        body = sm[:-1] if br else sm
+        n = len(body)
+        k_lo = n * len(qk) // max(1, len(mf)) + 1
+        fill = merge(body, [(i, x) for i, x in zip(spread(len(kr), k_lo, n * 3 // 4), kr)] +
+                     [(i, x) for i, x in zip(spread(len(dma), 4, n // 2), dma)])
+        # the V^T reads follow their P.V MFMAs (second half of the phase): after the softmax
+        fill += vr
+        if br:
+            br.not_before = len(mf)
+            fill.append(br)
+        return [mark()] + place(mf, fill)
+
+
+def par(t):
+    """Register buffer ('A' even / 'B' odd) of tile t in the 8-wave form."""
+    return 'A' if t % 2 == 0 else 'B'
 
 
 def mark():
@@ -1177,7 +1253,7 @@ def prologue(g):
     p += [V(f'v_lshrrev_b32 v33, {lpr.bit_length() - 1}, v{L}', 33, [L]), V(f'v_and_b32 v34, {lpr - 1}, v{L}', 34, [L]),
           S(f's_lshl_b32 s91, s{S_WAVE}, {rpp.bit_length() - 1}')]
     for i in range(NP):
-        p += [S(f's_add_u32 s92, s91, {4 * rpp * i}'), V('v_add_u32 v35, s92, v33', 35, [33])]
+        p += [S(f's_add_u32 s92, s91, {NWAVES * rpp * i}'), V('v_add_u32 v35, s92, v33', 35, [33])]
         p += xfun(36, 35, 37, 38)
         p += [V('v_xor_b32 v36, v34, v36', 36, [34, 36]), V('v_lshlrev_b32 v37, 3, v36', 37, [36]),
               V('v_cmp_gt_u32 vcc, s74, v37', 'vcc', [37]),
@@ -1187,10 +1263,10 @@ def prologue(g):
               Inst(f'v_cndmask_b32 v{V_DMA + NP + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'],
                    wr=[f'v{V_DMA + NP + i}'])]
     # Q load offsets (v43..v50), O store offsets, LSE offsets of blocks A (rows +0) and B (+32)
-    p += [S(f's_lshl_b32 s93, s{S_WAVE}, 6'), S('s_add_u32 s93, s93, s90')]
+    p += [S(f's_lshl_b32 s93, s{S_WAVE}, {(32 * len(BLOCKS)).bit_length() - 1}'), S('s_add_u32 s93, s93, s90')]
     # (O_BASE, head_dim == D: one row base per block, the chunk offsets as immediates)
     qoff = {'A': 43, 'B': 47} if not O_BASE else {'A': V_P['A'], 'B': V_P['A'] + 1}
-    for X, xo in (('A', 0), ('B', 32)):
+    for X, xo in (('A', 0), ('B', 32))[:len(BLOCKS)]:
         p += [V('v_add_u32 v39, s93, v16', 39, [16])]
         if xo:
             p += [V(f'v_add_u32 v39, {xo}, v39', 39, [39])]
@@ -1235,7 +1311,7 @@ def prologue(g):
     else:
         p += [Inst(f'v_accvgpr_write_b32 a{A_ONES + r}, v51', 'accw', rd=['v51'], wr=[f'a{A_ONES + r}']) for r in range(4)]
     # Q fragments
-    for X in 'AB':
+    for X in BLOCKS:
         for ks in range(NKS):
             q = A_Q[X] + 4 * ks
             qr, qi = (qoff[X], f' offset:{32 * ks}') if O_BASE else (qoff[X] + ks, '')
@@ -1261,10 +1337,14 @@ def prologue(g):
         p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in range(V_MCB['A'], V_MCB['B'] + 4)]
     p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
-    p += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier')]
+    # (8 waves: phase 0 reads K2 as well: K0 K1 V0 K2 landed, all but the 3 youngest pieces)
+    p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else 4 * (DIST - 1)})'), raw('s_barrier')]
     p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
     # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
     p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
+    if NWAVES == 8:
+        # K1 into the single K buffer behind QK(0) (phase 0 runs QK(1))
+        p += [raw('s_nop 3')] + g.kreads(1)
     p += [raw('s_nop 7'), raw('s_nop 3')]
     return p
 
@@ -1345,7 +1425,20 @@ def stamp_exit():
 def nvrel_insts():
     """Per-block key limits of a masked tile: NVREL_X = ROW1_X - 64 j."""
     return [S(f's_lshl_b32 s96, s{S_J}, 6')] + \
-           [V(f'v_subrev_u32 v{V_NVREL[X]}, s96, v{V_ROW1[X]}', V_NVREL[X], [V_ROW1[X]]) for X in 'AB']
+           [V(f'v_subrev_u32 v{V_NVREL[X]}, s96, v{V_ROW1[X]}', V_NVREL[X], [V_ROW1[X]]) for X in BLOCKS]
+
+
+def tile_vmcnt():
+    """vmcnt of the wait before each tile's barrier: the 4-wave form needs K(t+2), V(t+1) in LDS
+    for the next tile (all but the DMAs of the last DIST - 1 tiles); the 8-wave form reads K(t+2)
+    one tile earlier (all but this tile's two pieces)."""
+    return 2 * NP * (DIST - 2) if NWAVES == 8 else 4 * (DIST - 1)
+
+
+def tile_phases(g, t, **kw):
+    if NWAVES == 8:
+        return g.phase_w8(t, **kw)
+    return g.phase1(t, **kw) + g.phase2(t, **kw)
 
 
 def masked_tile(g, t, rescue):
@@ -1353,9 +1446,8 @@ def masked_tile(g, t, rescue):
     the last one, which exits to .Llast{t}."""
     blk = [label(f'.Lmask{t}'), S(f's_cmp_eq_u32 s{S_J}, s{S_LAST}'), raw(f's_cbranch_scc1 .Llast{t}')]
     blk += nvrel_insts()
-    blk += g.phase1(t, masked=True, rescue=rescue)
-    blk += g.phase2(t, masked=True, rescue=rescue)
-    blk += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier'), S(f's_add_u32 s{S_J}, s{S_J}, 1')]
+    blk += tile_phases(g, t, masked=True, rescue=rescue)
+    blk += [raw(f's_waitcnt vmcnt({tile_vmcnt()})'), raw('s_barrier'), S(f's_add_u32 s{S_J}, s{S_J}, 1')]
     if t == U - 1:
         blk.append(raw('s_branch .Lmask0'))
     return blk
@@ -1365,10 +1457,13 @@ def last_tile(g, t, rescue):
     """Tile t = nt - 1 (position t of the unrolled loop): masked softmax of both blocks, no
     next-tile reads or DMA, then P.V of block B and the two epilogues."""
     b = [label(f'.Llast{t}')] + (stamp(STAMP_V + 2) if 'stamps' in PROBE else []) + nvrel_insts()
-    b += g.phase1(t, masked=True, last=True, rescue=rescue)
-    b += g.phase2(t, masked=True, last=True, rescue=rescue)
-    b += [mark()] + place(g.pv_sum('B', t)[0], g.epilogue('A'))
-    b += [mark()] + g.epilogue('B')
+    b += tile_phases(g, t, masked=True, last=True, rescue=rescue)
+    if NWAVES == 8:
+        b += [mark()] + place(g.pv_sum(par(t), t)[0], [])
+        b += [mark()] + g.epilogue('A')
+    else:
+        b += [mark()] + place(g.pv_sum('B', t)[0], g.epilogue('A'))
+        b += [mark()] + g.epilogue('B')
     b += [raw('s_waitcnt vmcnt(0)')] + stamp_exit() + [raw('s_endpgm')]
     return b
 
@@ -1385,21 +1480,24 @@ def build(g):
             blk.append(raw('.p2align 6'))
             blk.append(label('.Lloop'))
         blk += [S(f's_cmp_ge_u32 s{S_J}, s{S_MSTART}'), raw(f's_cbranch_scc1 .Lmask{t}')]
-        blk += g.phase1(t, rescue=rescue)
-        if DUMP and DUMP[0] == 'p1' and t == 0:
-            blk += dump_block(DUMP[1])
-        blk += g.phase2(t, rescue=rescue)
-        if DUMP and DUMP[0] == 'p2' and t == 0:
-            blk += dump_block(DUMP[1])
+        if NWAVES == 8:
+            blk += g.phase_w8(t, rescue=rescue)
+        else:
+            blk += g.phase1(t, rescue=rescue)
+            if DUMP and DUMP[0] == 'p1' and t == 0:
+                blk += dump_block(DUMP[1])
+            blk += g.phase2(t, rescue=rescue)
+            if DUMP and DUMP[0] == 'p2' and t == 0:
+                blk += dump_block(DUMP[1])
         if 'nobar' not in PROBE:
-            blk += [raw(f's_waitcnt vmcnt({4 * (DIST - 1)})'), raw('s_barrier')]
+            blk += [raw(f's_waitcnt vmcnt({tile_vmcnt()})'), raw('s_barrier')]
         blk += [S(f's_add_u32 s{S_J}, s{S_J}, 1')]
         if t == U - 1:
             blk.append(raw('s_branch .Lloop'))
         tiles.append(blk)
     masks = [masked_tile(g, t, rescue) for t in range(U)]
     lasts = [last_tile(g, t, rescue) for t in range(U)]
-    empty = [label('.Lempty'), mark()] + g.epilogue('A') + [mark()] + g.epilogue('B') + \
+    empty = [label('.Lempty')] + sum(([mark()] + g.epilogue(X) for X in BLOCKS), []) + \
             [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
     end = [label('.Lend'), raw('s_endpgm')]
     # control-flow paths for the hazard pass
@@ -1472,7 +1570,7 @@ def emit(g, blocks):
               '    .args:', '      - .offset: 0', f'        .size: {KARG_BYTES}', '        .value_kind: by_value',
               f'    .group_segment_fixed_size: {LDS_BYTES}',
               '    .kernarg_segment_align: 8', f'    .kernarg_segment_size: {KARG_BYTES}',
-              '    .max_flat_workgroup_size: 256', f'    .name: {name}',
+              f'    .max_flat_workgroup_size: {64 * NWAVES}', f'    .name: {name}',
               '    .private_segment_fixed_size: 0', f'    .sgpr_count: {NSGPR + 2}',
               f'    .symbol: {name}.kd', f'    .vgpr_count: {NVGPR + NAGPR}', '    .wavefront_size: 64',
               'amdhsa.target: amdgcn-amd-amdhsa--gfx950', 'amdhsa.version:', '  - 1', '  - 2', '...',
@@ -1500,6 +1598,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f16'])
     ap.add_argument('--hd', type=int, default=64, choices=[64, 128], help='head-dim tile')
+    ap.add_argument('--waves', type=int, default=4, choices=[4, 8], help='waves per workgroup (8: D = 64 only)')
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats', action='store_true')
     ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')
@@ -1519,7 +1618,7 @@ def main():
         pt, regs = args.dump.split(':')
         DUMP = (pt, expand_regs(regs))
     PROBE.update(x for x in args.probe.split(',') if x)
-    configure(args.hd)
+    configure(args.hd, args.waves)
     global VREADS_P1, SM_PIPE
     if args.ring or args.dist:
         set_geometry(args.ring or R, args.dist or DIST)

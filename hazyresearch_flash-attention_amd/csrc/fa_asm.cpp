@@ -26,6 +26,10 @@ extern const unsigned char fa_asm_fwd_d128_bf16[];
 extern const unsigned long fa_asm_fwd_d128_bf16_size;
 extern const unsigned char fa_asm_fwd_d128_f16[];
 extern const unsigned long fa_asm_fwd_d128_f16_size;
+extern const unsigned char fa_asm_fwd_d64w8_bf16[];
+extern const unsigned long fa_asm_fwd_d64w8_bf16_size;
+extern const unsigned char fa_asm_fwd_d64w8_f16[];
+extern const unsigned long fa_asm_fwd_d64w8_f16_size;
 }
 
 namespace fa {
@@ -66,27 +70,29 @@ constexpr int kRows = 256;            // query rows per workgroup
 constexpr int kMaxDev = 64;
 constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
 
-// kernels: [d-tile (0: 64, 1: 128) * 2 + dtype (0: bf16, 1: f16)]
+// kernels: [form (0: D=64, 1: D=128, 2: D=64 two waves per SIMD) * 2 + dtype (0: bf16, 1: f16)]
+constexpr int kNumFns = 6;
 struct DevFns {
-    hipModule_t mod[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipFunction_t fn[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipModule_t mod[kNumFns] = {};
+    hipFunction_t fn[kNumFns] = {};
 };
 std::mutex g_mu;
 DevFns g_fns[kMaxDev];
 
-hipError_t get_function(int dtype, int hd, hipFunction_t *out) {
+hipError_t get_function(int dtype, int form, hipFunction_t *out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
-    const int k = (hd == 128 ? 2 : 0) + (dtype == FA_DTYPE_BF16 ? 0 : 1);
+    const int k = 2 * form + (dtype == FA_DTYPE_BF16 ? 0 : 1);
     std::lock_guard<std::mutex> lk(g_mu);
     DevFns &d = g_fns[dev];
     if (!d.fn[k]) {
-        static const void *const imgs[4] = {fa_asm_fwd_d64_bf16, fa_asm_fwd_d64_f16, fa_asm_fwd_d128_bf16,
-                                            fa_asm_fwd_d128_f16};
-        static const char *const names[4] = {"fa_fwd_d64_bf16_asm", "fa_fwd_d64_f16_asm", "fa_fwd_d128_bf16_asm",
-                                             "fa_fwd_d128_f16_asm"};
+        static const void *const imgs[kNumFns] = {fa_asm_fwd_d64_bf16, fa_asm_fwd_d64_f16, fa_asm_fwd_d128_bf16,
+                                                  fa_asm_fwd_d128_f16, fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16};
+        static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm", "fa_fwd_d64_f16_asm",
+                                                   "fa_fwd_d128_bf16_asm", "fa_fwd_d128_f16_asm",
+                                                   "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm"};
         const void *img = imgs[k];
         const char *name = names[k];
         e = hipModuleLoadData(&d.mod[k], img);
@@ -128,9 +134,17 @@ bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
     return true;
 }
 
+// The two-waves-per-SIMD form (8-wave workgroups, one 32-row block per wave) serves head_dim == 64
+// only (its Q loads and O stores address whole rows from one base).
+static bool use_w8(const FaFwdArgs &a) {
+    if (a.head_dim != 64 || a.impl == FA_IMPL_ASM4) return false;
+    return a.impl == FA_IMPL_ASM8;
+}
+
 hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
     hipFunction_t fn = nullptr;
-    hipError_t e = get_function(a.dtype, a.head_dim > 64 ? 128 : 64, &fn);
+    const bool w8 = use_w8(a);
+    hipError_t e = get_function(a.dtype, w8 ? 2 : (a.head_dim > 64 ? 1 : 0), &fn);
     if (e != hipSuccess) return e;
     FaAsmFwdArgs k;
     std::memset(&k, 0, sizeof(k));
@@ -176,7 +190,8 @@ hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
     }
     size_t size = sizeof(k);
     void *config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
-    e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, kRows, 1, 1, 0, stream, nullptr, config);
+    e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, w8 ? 2 * kRows : kRows, 1, 1, 0, stream,
+                              nullptr, config);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

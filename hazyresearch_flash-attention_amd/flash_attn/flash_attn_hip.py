@@ -73,6 +73,8 @@ class FaFwdArgs(ctypes.Structure):
 
 FA_IMPL_AUTO = 0
 FA_IMPL_HIP = 1
+FA_IMPL_ASM4 = 2    # the one-wave-per-SIMD assembly forward where eligible (tests, A/B)
+FA_IMPL_ASM8 = 3    # the two-waves-per-SIMD assembly forward where eligible (head_dim == 64)
 
 
 class FaBwdArgs(ctypes.Structure):

@@ -24,19 +24,19 @@ from oracle.attention_ref import attention_ref  # noqa: E402
 _TXT = {}
 
 
-def _kernel(dtype, hd=64):
-    if (dtype, hd) not in _TXT:
-        gen_fwd.configure(hd)
+def _kernel(dtype, hd=64, waves=4):
+    if (dtype, hd, waves) not in _TXT:
+        gen_fwd.configure(hd, waves)
         try:
             g = gen_fwd.Gen(dtype)
             blocks, _ = gen_fwd.build(g)
-            _TXT[(dtype, hd)] = gen_fwd.emit(g, blocks)
+            _TXT[(dtype, hd, waves)] = gen_fwd.emit(g, blocks)
         finally:
             gen_fwd.configure(64)
-    return _TXT[(dtype, hd)]
+    return _TXT[(dtype, hd, waves)]
 
 
-def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False):
+def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4):
     rng = np.random.default_rng(seed)
     cv = asm_sim.bf16_bits if dtype == "bf16" else asm_sim.f16_bits
     B, tq, tk = len(lens_q), sum(lens_q), sum(lens_k)
@@ -66,7 +66,7 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False):
                        nqb, nqb * H * B, mg(nqb), mg(H), D, H * B, int(causal), mg(H * B),
                        per, mg(per) if per else 0, grp, mg(grp) if grp else 0)
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
-    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64), dtype).run((nqb, H, B), pa, mem)
+    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64, waves), dtype).run((nqb, H, B), pa, mem)
     o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
     lse = mem.get(pl).view(np.float32).reshape(B, H, lse_stride)
     to = lambda x: torch.from_numpy(asm_sim.from16(x.astype(np.uint32), dtype))
@@ -146,8 +146,8 @@ def test_asm_forward_rescale_path_in_simulator():
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("hd", [64, 128])
-def test_generated_kernel_assembles(dtype, hd, tmp_path):
+@pytest.mark.parametrize("hd,waves", [(64, 4), (128, 4), (64, 8)])
+def test_generated_kernel_assembles(dtype, hd, waves, tmp_path):
     """The simulator does not check encodings (register alignment, gfx950 operand forms): the
     product kernels must also assemble for gfx950, as build.py does."""
     import subprocess
@@ -155,7 +155,25 @@ def test_generated_kernel_assembles(dtype, hd, tmp_path):
     if not os.path.exists(llvm):
         pytest.skip("no ROCm LLVM")
     s = tmp_path / "k.s"
-    s.write_text(_kernel(dtype, hd))
+    s.write_text(_kernel(dtype, hd, waves))
     r = subprocess.run([llvm, "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c", str(s),
                         "-o", str(tmp_path / "k.o")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("lens_q,lens_k,causal", [
+    ([130], [200], False),            # 3 full tiles + a masked one, rows past the block end
+    ([257, 40], [33, 190], False),    # var-len, two q-blocks, single masked tile
+    ([70], [700], False),             # 11 tiles: every unrolled loop position and its last-tile exit
+    ([40, 64], [0, 65], False),       # empty key set (zeros, -inf)
+    ([300], [300], True),             # causal: the diagonal band of two q-blocks
+])
+def test_asm_forward_w8_in_simulator(lens_q, lens_k, causal, dtype):
+    """The two-waves-per-SIMD form (8 waves, one 32-row block per wave, head_dim == 64)."""
+    _run(lens_q, lens_k, 1, 64, dtype, causal=causal, waves=8)
+
+
+def test_asm_forward_w8_rescale_path_in_simulator():
+    """The 8-wave form's rescale block runs after the phase's P.V MFMAs into the same O."""
+    _run([70], [300], 1, 64, "bf16", scale=3.0, waves=8)

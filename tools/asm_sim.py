@@ -118,6 +118,7 @@ class Sim:
         m = re.search(r'\.amdhsa_accum_offset (\d+)', asm_text)
         self.nv = int(m.group(1))
         self.lds_bytes = int(re.search(r'\.amdhsa_group_segment_fixed_size (\d+)', asm_text).group(1))
+        self.nwaves = int(re.search(r'\.max_flat_workgroup_size: (\d+)', asm_text).group(1)) // 64
         self.count = {}
 
     @staticmethod
@@ -231,7 +232,7 @@ class Sim:
     def run_wg(self, wg, karg, mem, max_steps):
         self.mem, self.karg = mem, karg
         self.lds = np.zeros(self.lds_bytes, dtype=np.uint8)
-        waves = [Wave(self.nv, 256, i, wg) for i in range(4)]
+        waves = [Wave(self.nv, 256, i, wg) for i in range(self.nwaves)]
         for w in waves:
             w.s[0] = karg & 0xFFFFFFFF
             w.s[1] = karg >> 32

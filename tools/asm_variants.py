@@ -31,7 +31,10 @@ def build(spec, out_dir):
     subprocess.check_call([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
                            s, "-o", s[:-2] + ".o"])
     subprocess.check_call([f"{LLVM}/ld.lld", "-shared", s[:-2] + ".o", "-o", s[:-2] + ".hsaco"])
-    return open(s[:-2] + ".hsaco", "rb").read()
+    txt = open(s).read()
+    name = txt.split(".globl ")[1].split()[0]
+    threads = int(txt.split(".max_flat_workgroup_size: ")[1].split()[0])
+    return open(s[:-2] + ".hsaco", "rb").read(), name, threads
 
 
 def main():
@@ -61,9 +64,12 @@ def main():
     nqb = (S + 255) // 256
     mg = lambda d: ((1 << 32) + 2 * d - 1) // (2 * d)
     c = np.float32(D ** -0.5 * 1.4426950408889634)
-    kb = struct.pack("<7Q4Q4I2I2f2I2I2I", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
-                     cu.data_ptr(), cu.data_ptr(), D * 2, D * 2, D * 2, D * 2, H * D * 2, H * D * 2, H * D * 2,
-                     H * D * 2, H, lse_stride * 4, c, np.float32(8.0 / c), nqb, nqb * H * B, mg(nqb), mg(H), D, 0)
+    # the whole 168-byte argument block of fa_asm.cpp (FaAsmFwdArgs), non-causal
+    kb = struct.pack("<7Q4Q4I2I2f2I2I2I2I4I", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                     lse.data_ptr(), cu.data_ptr(), cu.data_ptr(), D * 2, D * 2, D * 2, D * 2, H * D * 2, H * D * 2,
+                     H * D * 2, H * D * 2, H, lse_stride * 4, c, np.float32(8.0 / c), nqb, nqb * H * B, mg(nqb),
+                     mg(H), D, H * B, 0, mg(H * B), 0, 0, 0, 0)
+    assert len(kb) == 168
     libs = [ln.split()[-1] for ln in open("/proc/self/maps").read().split("\n") if "libamdhip64" in ln]
     hip = ctypes.CDLL(libs[0])
     kbuf = ctypes.create_string_buffer(kb, len(kb))
@@ -71,20 +77,34 @@ def main():
     extra = (ctypes.c_void_p * 5)(1, ctypes.addressof(kbuf), 2, ctypes.addressof(size), 3)
     fns = {}
     keep = []
-    for name, img in images.items():
+    threads = {}
+    for name, (img, kname, nthr) in images.items():
         mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
         buf = ctypes.create_string_buffer(img, len(img))
         keep.append(buf)
         assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
-        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"fa_fwd_d64_bf16_asm") == 0
+        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, kname.encode()) == 0
         fns[name] = fn
+        threads[fn.value] = nthr
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def launch(fn):
-        rc = hip.hipModuleLaunchKernel(fn, nqb, H, B, 256, 1, 1, 0, stream, None, extra)
+        rc = hip.hipModuleLaunchKernel(fn, nqb, H, B, threads[fn.value], 1, 1, 0, stream, None, extra)
         assert rc == 0
 
     flops = 4.0 * B * H * S * S * D
+    # correctness of every variant on sequence 0 (probe variants are wrong by design)
+    qf, kf, vf = (x[:S].float().transpose(0, 1) for x in (q, k, v))
+    sc = torch.matmul(qf, kf.transpose(1, 2)) * D ** -0.5
+    ref = torch.matmul(torch.softmax(sc, -1), vf).transpose(0, 1)
+    ref_lse = torch.logsumexp(sc, -1)
+    for n in variants:
+        o.zero_()
+        launch(fns[n])
+        torch.cuda.synchronize()
+        err = (o[:S].float() - ref).abs().max().item()
+        lerr = (lse[0, :, :S] - ref_lse).abs().max().item()
+        print(f"check {(n.split(':')[0] if n else 'base'):24s} max|o-ref| {err:.3e}  max|lse-ref| {lerr:.3e}", flush=True)
     # warm the clock
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:
