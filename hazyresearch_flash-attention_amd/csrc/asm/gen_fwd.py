@@ -121,6 +121,7 @@ BLOCKS = 'AB'          # 32-row query blocks of a wave
 NETMP = 16             # rotating exp temporaries
 V_ORT = None           # OR-test accumulator (None: V_TMP[X])
 V_EPT = None           # epilogue temporaries (None: V_TMP[X])
+PRIO4 = False          # 8 waves: s_setprio 1 for waves 4-7 (the SIMD partners dispatched second)
 
 
 def rq(base):
@@ -1345,6 +1346,9 @@ def prologue(g):
     if NWAVES == 8:
         # K1 into the single K buffer behind QK(0) (phase 0 runs QK(1))
         p += [raw('s_nop 3')] + g.kreads(1)
+        if PRIO4:
+            p += [S(f's_cmp_lt_u32 s{S_WAVE}, 4'), raw('s_cbranch_scc1 .Lprio_done'), raw('s_setprio 1'),
+                  label('.Lprio_done')]
     p += [raw('s_nop 7'), raw('s_nop 3')]
     return p
 
@@ -1599,6 +1603,7 @@ def main():
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f16'])
     ap.add_argument('--hd', type=int, default=64, choices=[64, 128], help='head-dim tile')
     ap.add_argument('--waves', type=int, default=4, choices=[4, 8], help='waves per workgroup (8: D = 64 only)')
+    ap.add_argument('--prio4', type=int, default=None, help='8 waves: s_setprio 1 for waves 4-7')
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats', action='store_true')
     ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')
@@ -1638,6 +1643,9 @@ def main():
         EXP_LAG, CVT_LAG = (int(x) for x in args.lag.split(','))
     if args.mcbanks is not None:
         MC_BANKS = bool(args.mcbanks)
+    global PRIO4
+    if args.prio4 is not None:
+        PRIO4 = bool(args.prio4)
     if MC_BANKS:
         NVGPR = max(NVGPR, V_MCB['B'] + 4)
     global KARG_BYTES
