@@ -36,6 +36,7 @@ cdna_hip_programming.md (Appendix B, "4-wave, one-wave-per-SIMD") describes:
 Nothing here writes through the scalar data cache: all stores are vector buffer stores.
 """
 import argparse
+import copy
 import math
 import os
 import sys
@@ -151,6 +152,7 @@ def configure(hd, waves=4):
     global NWAVES, BLOCKS, NETMP, V_ORT, V_EPT, EXP_LAG, CVT_LAG
     assert hd in (64, 128) and waves in (4, 8)
     globals().update(_D64)   # the D = 64 layout, then the D = 128 / 8-wave changes
+    globals().update(PERSIST=False, KARG_BYTES=168)
     EXP_LAG, CVT_LAG = 4, 4
     if waves == 8:
         assert hd == 64
@@ -300,7 +302,7 @@ class Gen:
         self.cvt = 'v_cvt_pk_bf16_f32' if dtype == 'bf16' else 'v_cvt_pk_f16_f32'
         self.one2 = 0x3F803F80 if dtype == 'bf16' else 0x3C003C00
         self.nlabel = 0
-        self.name = f'fa_fwd_d{D}{"w8" if NWAVES == 8 else ""}_{dtype}_asm'
+        self.name = f'fa_fwd_d{D}{"w8" if NWAVES == 8 else ""}{"p" if PERSIST else ""}_{dtype}_asm'
 
     def lab(self, stem):
         self.nlabel += 1
@@ -386,7 +388,7 @@ class Gen:
             return []
         return self._dma(kind, t)
 
-    def _dma(self, kind, t):
+    def _dma(self, kind, t, nxt=False, walk_only=False):
         """This wave's two 1-KiB pieces of the K or V tile t (LDS-DMA into ring slot t % R).
         Tile t reads through descriptor set t % 2. Each set walks the sequence two tiles at a
         time: right before its next use its base advances by 128 rows and num_records shrinks by
@@ -397,6 +399,8 @@ class Gen:
         out = []
         region = KREG if kind == 'K' else VREG
         desc = (S_KD if t % 2 == 0 else S_KD1) if kind == 'K' else (S_VD if t % 2 == 0 else S_VD1)
+        if nxt:     # the next block's sets (persistent form's tail: t = the next block's tile)
+            desc = S_NXD[kind][t % 2]
         step = S_KSTEP if kind == 'K' else S_VSTEP          # 2 tiles of bytes
         dregs = [f's{desc + i}' for i in range(4)]
         if t >= 2 and 'nowalk' not in PROBE:
@@ -405,6 +409,8 @@ class Gen:
             out.append(salu(f's_addc_u32 s{desc + 1}, s{desc + 1}, 0', rd=[dregs[1], 'scc'], wr=[dregs[1], 'scc']))
             out.append(salu(f's_sub_u32 s{desc + 2}, s{desc + 2}, {st}', rd=[dregs[2], st], wr=[dregs[2], 'scc']))
             out.append(salu(f's_cselect_b32 s{desc + 2}, 0, s{desc + 2}', rd=[dregs[2], 'scc'], wr=[dregs[2]]))
+        if walk_only:
+            return out
         for i in range(NP):
             m0 = region + (t % R) * TILE + 1024 * NWAVES * i   # + 1024 * wave (S_M0B)
             voff = V_DMA + (0 if kind == 'K' else NP) + i
@@ -693,8 +699,9 @@ class Gen:
         e.append(V(f'v_mul_f32 v{T + 3}, 0x3f317218, v{T + 3}', T + 3, [T + 3]))
         e.append(Inst(f'v_cndmask_b32 v{T + 3}, v{T + 3}, v{V_NEGINF}, vcc', 'valu', rd=[f'v{T + 3}', f'v{V_NEGINF}', 'vcc'],
                       wr=[f'v{T + 3}']))
-        e.append(Inst(f'buffer_store_dword v{T + 3}, v{V_LOFF[X]}, s[{S_LD}:{S_LD + 3}], 0 offen', 'vstore', 8,
-                      rd=[f'v{T + 3}', f'v{V_LOFF[X]}']))
+        if 'noepi' not in PROBE:     # timing probe: no LSE / O stores (the store tail's price)
+            e.append(Inst(f'buffer_store_dword v{T + 3}, v{V_LOFF[X]}, s[{S_LD}:{S_LD + 3}], 0 offen', 'vstore', 8,
+                          rd=[f'v{T + 3}', f'v{V_LOFF[X]}']))
         for dt in range(NDT):
             for gi, g in enumerate((0, 2)):
                 # registers 4g..4g+7 of d-block dt hold d = 8g + 4hi + 0..3 and 8(g+1) + 4hi + 0..3
@@ -719,12 +726,13 @@ class Gen:
                     oreg, oimm = V_OOFF[X], f' offset:{16 * (4 * dt + g)}'
                 else:
                     oreg, oimm = V_OOFF[X] + dt * 2 + gi, ''
-                e.append(Inst(f'buffer_store_dwordx4 {vs(Wb, 4)}, v{oreg}, s[{S_OD}:{S_OD + 3}], 0 offen{oimm}',
-                              'vstore', 8, rd=rv(Wb, 4) + [f'v{oreg}']))
+                if 'noepi' not in PROBE:
+                    e.append(Inst(f'buffer_store_dwordx4 {vs(Wb, 4)}, v{oreg}, s[{S_OD}:{S_OD + 3}], 0 offen{oimm}',
+                                  'vstore', 8, rd=rv(Wb, 4) + [f'v{oreg}']))
         return e
 
     # ------------------------------------------------------------------ phases
-    def phase1(self, t, masked=False, last=False, rescue=None):
+    def phase1(self, t, masked=False, last=False, rescue=None, kv_next=False):
         """Tile t, phase 1: QK_B(t) + PV_B(t-1) + row sums beside block A's softmax of tile t,
         K(t+1) fragment reads and the K(t+1+DIST) DMA."""
         qkb = self.qk('B', t)
@@ -741,11 +749,13 @@ class Gen:
         if VREADS_P1:
             side = [x for _, x in self.vreads(t)] + side
         dma = [] if (last or DMA_P2) else self.dma('K', t + 1 + DIST)
+        if kv_next:     # tail tile t (block tile nt - 4 + t) loads K(nt + t) = the next block's K(t)
+            dma = self._dma('K', t, nxt=True)
         fill = merge(sm, [(i, x) for i, x in zip(spread(len(side), k_lo, len(sm) - 4), side)] +
                      [(i, x) for i, x in zip(spread(len(dma), 6, len(sm) - 10), dma)])
         return [mark()] + place(mf, fill)
 
-    def phase2(self, t, masked=False, last=False, rescue=None):
+    def phase2(self, t, masked=False, last=False, rescue=None, kv_next=False):
         """Tile t, phase 2: QK_A(t+1) + PV_A(t) + row sums beside block B's softmax of tile t,
         V(t) fragment reads (deadline: 3 MFMAs before their P.V MFMA) and the V(t+DIST) DMA."""
         qk = [] if last else self.qk('A', t + 1)
@@ -757,6 +767,8 @@ class Gen:
             ins.deadline = max(0, len(qk) + use[f] - 3)
             vr.append(ins)
         dma = [] if last else self.dma('V', t + DIST)
+        if kv_next:     # V(nt - 1 + t): this block's last V tile, then the next block's V(t - 1)
+            dma = self.dma('V', t + DIST) if t == 0 else self._dma('V', t - 1, nxt=True)
         if DMA_P2 and not last:
             dma = self.dma('K', t + 1 + DIST) + dma
         # the V reads go early (two per softmax instruction pair), the DMA pieces in the middle
@@ -1140,7 +1152,16 @@ def wave_id_insts():
             Inst(f'v_readfirstlane_b32 s{S_WAVE}, v1', 'rfl', rd=['v1'], wr=[f's{S_WAVE}'])]
 
 
+def sec(name):
+    """Section marker inside the prologue list (prologue_sections splits on them)."""
+    return Inst(name, 'sec', 0)
+
+
 def prologue(g):
+    return [x for x in prologue_sections(g) if x.kind != 'sec']
+
+
+def prologue_sections(g):
     """Kernel arguments, (q-block, head, batch) of this workgroup (XCD-aware order as
     fa_fwd_kernel.h), sequence bounds, buffer descriptors, per-lane addresses, Q loads, the first
     DMAs, zeroed accumulators, and QK_A of tile 0."""
@@ -1159,9 +1180,10 @@ def prologue(g):
     p.append(raw('s_waitcnt lgkmcnt(0)'))
     if WAVE_MODE == 'early':
         p += wave_id_insts()
+    p.append(sec('decode'))
     # L = x + nqb (y + H z); Lp = xcd q8 + min(xcd, r8) + (L >> 3); bh = Lp / nqb; b = bh / H
     p += [S('s_mul_i32 s80, s66, s4'), S('s_add_u32 s80, s80, s3'), S('s_mul_i32 s80, s80, s70'),
-          S('s_add_u32 s80, s80, s2'),
+          S('s_add_u32 s80, s80, s2'), sec('decode_map'),
           S('s_and_b32 s81, s80, 7'), S('s_lshr_b32 s82, s71, 3'), S('s_and_b32 s83, s71, 7'),
           S('s_mul_i32 s84, s81, s82'), S('s_min_u32 s85, s81, s83'), S('s_add_u32 s84, s84, s85'),
           S('s_lshr_b32 s85, s80, 3'), S('s_add_u32 s84, s84, s85'),
@@ -1193,8 +1215,10 @@ def prologue(g):
           S('s_add_u32 s94, s52, s90'), S('s_addc_u32 s95, s53, 0'),
           Inst('s_load_dwordx2 s[78:79], s[94:95], 0x0', 'smem', 2, wr=['s78', 's79']),
           raw('s_waitcnt lgkmcnt(0)')]
+    p.append(sec('wave'))
     if WAVE_MODE != 'early':
         p += wave_id_insts()
+    p.append(sec('state'))
     p += [S('s_sub_u32 s77, s77, s76'), S('s_sub_u32 s79, s79, s78'),
           S('s_lshl_b32 s90, s87, 8'), S('s_cmp_ge_u32 s90, s77'), raw('s_cbranch_scc1 .Lend')]
     # descriptors: K, V, Q, O, LSE
@@ -1224,6 +1248,7 @@ def prologue(g):
               S(f's_sub_u32 s{d1 + 2}, s{d0 + 2}, s96'), S(f's_cselect_b32 s{d1 + 2}, 0, s{d1 + 2}'),
               S(f's_mov_b32 s{d1 + 3}, s{d0 + 3}')]
     # ---- per-lane constants
+    p.append(sec('lanes'))
     L = V_LANE
     p += [V(f'v_and_b32 v{L}, 63, v0', L, [0]), V('v_and_b32 v16, 31, v0', 16, [0]),
           V('v_bfe_u32 v17, v0, 5, 1', 17, [0]), V('v_bfe_u32 v18, v0, 2, 2', 18, [0]),
@@ -1264,6 +1289,7 @@ def prologue(g):
               Inst(f'v_cndmask_b32 v{V_DMA + NP + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'],
                    wr=[f'v{V_DMA + NP + i}'])]
     # Q load offsets (v43..v50), O store offsets, LSE offsets of blocks A (rows +0) and B (+32)
+    p.append(sec('rows'))
     p += [S(f's_lshl_b32 s93, s{S_WAVE}, {(32 * len(BLOCKS)).bit_length() - 1}'), S('s_add_u32 s93, s93, s90')]
     # (O_BASE, head_dim == D: one row base per block, the chunk offsets as immediates)
     qoff = {'A': 43, 'B': 47} if not O_BASE else {'A': V_P['A'], 'B': V_P['A'] + 1}
@@ -1300,6 +1326,7 @@ def prologue(g):
               Inst(f'v_cndmask_b32 v{V_LOFF[X]}, v31, v42, vcc', 'valu', rd=['v31', 'v42', 'vcc'],
                    wr=[f'v{V_LOFF[X]}'])]
     # ds_bpermute addresses and the 0/1 indicator of the row-sum MFMA
+    p.append(sec('lanes2'))
     p += [V(f'v_and_b32 v40, 15, v{L}', 40, [L]), V(f'v_lshrrev_b32 v41, 5, v{L}', 41, [L]),
           V('v_lshl_or_b32 v41, v41, 4, v40', 41, [41, 40]), V(f'v_lshlrev_b32 v{V_BPA}, 2, v41', V_BPA, [41]),
           V(f'v_bfe_u32 v41, v{L}, 4, 1', 41, [L]), V('v_lshl_add_u32 v41, v41, 5, v40', 41, [41, 40]),
@@ -1311,19 +1338,26 @@ def prologue(g):
         p += [V(f'v_mov_b32 v{A_ONES + r}, v51', A_ONES + r, [51]) for r in range(4)]
     else:
         p += [Inst(f'v_accvgpr_write_b32 a{A_ONES + r}, v51', 'accw', rd=['v51'], wr=[f'a{A_ONES + r}']) for r in range(4)]
-    # Q fragments
-    for X in BLOCKS:
+    # Q fragments ('nopro' timing probe: no Q loads and no first DMAs, the prologue burst's price)
+    p.append(sec('qload'))
+    for X in ([] if 'nopro' in PROBE else BLOCKS):
         for ks in range(NKS):
             q = A_Q[X] + 4 * ks
             qr, qi = (qoff[X], f' offset:{32 * ks}') if O_BASE else (qoff[X] + ks, '')
             p.append(Inst(f'buffer_load_dwordx4 {rq(q)}, v{qr}, s[{S_QD}:{S_QD + 3}], 0 offen{qi}', 'vload', 8,
                           rd=[f'v{qr}'], wr=rqn(q)))
     # first DMAs: K0, [K1 V0], [K2 V1], [K3 V2] (tile t of the loop issues K(t+1+DIST), V(t+DIST))
-    p += g.dma('K', 0)
-    for t in range(DIST):
-        p += g.dma('K', t + 1) + g.dma('V', t)
+    p.append(sec('dma'))
+    if 'nopro' in PROBE:     # Q = 0 (S = 0: one rescale at tile 0, as always, then none)
+        p += [Inst(f'v_accvgpr_write_b32 a{A_Q[X] + r}, 0', 'accw', wr=[f'a{A_Q[X] + r}'])
+              for X in BLOCKS for r in range(4 * NKS)] if not QL_VGPR else []
+    if 'nopro' not in PROBE:
+        p += g.dma('K', 0)
+        for t in range(DIST):
+            p += g.dma('K', t + 1) + g.dma('V', t)
     # zero O, row sums, the V fragment buffer PV_B(-1) reads and P_B (PV_B(-1) of tile 0 adds
     # nothing); m = -inf
+    p.append(sec('zero'))
     if QL_VGPR:
         p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(D)]
         p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(A_L['A'], A_L['B'] + 4)]
@@ -1336,6 +1370,7 @@ def prologue(g):
     p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in (V_MTHR['A'], V_MTHR['B'], V_MC['A'], V_MC['B'])]
     if MC_BANKS:
         p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in range(V_MCB['A'], V_MCB['B'] + 4)]
+    p.append(sec('start'))
     p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
     # (8 waves: phase 0 reads K2 as well: K0 K1 V0 K2 landed, all but the 3 youngest pieces)
@@ -1351,6 +1386,153 @@ def prologue(g):
                   label('.Lprio_done')]
     p += [raw('s_nop 7'), raw('s_nop 3')]
     return p
+
+
+def split_sections(lst):
+    out, cur = {'args': []}, 'args'
+    for x in lst:
+        if x.kind == 'sec':
+            cur = x.txt
+            out[cur] = []
+        else:
+            out[cur].append(x)
+    return out
+
+
+# ---- persistent form (PERSIST): one workgroup per CU walks logical blocks L = P, P + G, P + 2G, ...
+# (the same XCD-aware block order as the one-block-per-workgroup launch), and prefetches the next
+# block's Q fragments into spare VGPRs while the current block runs, so that only the first block
+# of a workgroup pays the Q part of the prologue's load burst (probe 'nopro': the burst is ~15 %
+# of the north star's time).
+PERSIST = False
+S_L, S_G, S_QPF = 99, 100, 101      # logical block, grid size, "next Q prefetched" flag
+S_NQD = 4                           # next block's Q descriptor s[4:7] (1-D grid: s3, s4 unused)
+S_NQB = 3                           # next block's q-block index
+V_QN = 168                          # next Q fragments: v168.. (16 per block, A_Q layout)
+V_QNOFF = 200                       # next Q lane offsets (4 per block)
+V_TID = 208                         # workitem id kept across blocks
+NVGPR_PERSIST = 212
+S_NXD = {'K': (88, 92), 'V': (76, 4)}   # next block's K / V descriptor sets (even, odd tiles), tail only
+S_TAIL = 7                           # tile index where the tail starts (nt - 4), or -1
+
+
+def tail_blocks(g, rescue):
+    """Persistent form, block tiles nt-4 .. nt-1 (loop positions 0..3, nt % 4 == 0): the main loop's
+    and the last tile's code with the DMAs redirected to the next block's K0..K3 / V0..V2 (ring slots
+    0..3, as its prologue would have loaded them), then .Lseam with s101 = 2."""
+    b = [label('.Ltail')] + tail_desc()
+    for t in range(3):
+        b += g.phase1(t, rescue=rescue, kv_next=True) + g.phase2(t, rescue=rescue, kv_next=True)
+        b += [raw(f's_waitcnt vmcnt({tile_vmcnt()})'), raw('s_barrier'), S(f's_add_u32 s{S_J}, s{S_J}, 1')]
+    b += nvrel_insts()
+    b += g.phase1(3, masked=True, last=True, rescue=rescue, kv_next=True)
+    b += g.phase2(3, masked=True, last=True, rescue=rescue, kv_next=True)
+    b += [mark()] + place(g.pv_sum('B', 3)[0], g.epilogue('A'))
+    b += [mark()] + g.epilogue('B')
+    b += [S('s_mov_b32 s101, 2'), raw('s_branch .Lseam')]
+    return b
+
+
+def set_persist(on):
+    """Persistent form on/off (D = 64, 4 waves): 8 more kernel-argument bytes (grid size at 168),
+    registers up to V_TID."""
+    global PERSIST, KARG_BYTES, NVGPR
+    if on:
+        assert D == 64 and NWAVES == 4 and not MC_BANKS
+        NVGPR = max(NVGPR, NVGPR_PERSIST)
+        KARG_BYTES = 176
+    else:
+        KARG_BYTES = 168
+    PERSIST = on
+
+
+def prologue_persist(g):
+    """Blocks of the persistent prologue: (pro_a, pb1, qcopy, qload, pb2)."""
+    sc = split_sections(prologue_sections(g))
+    pro_a = sc['args'] + [Inst('s_load_dword s100, s[0:1], 0xa8', 'smem', 2, wr=['s100']),
+                          raw('s_waitcnt lgkmcnt(0)'),
+                          S('s_mov_b32 s99, s2'), S('s_mov_b32 s101, 0'), S('s_mov_b32 s98, 0'),
+                          V(f'v_mov_b32 v{V_TID}, v0', V_TID, [0])]
+    pro_a += sc['wave'] + sc['lanes'] + sc['lanes2']
+    # next block (clamped to the last one: its decode stays in range) -> Q descriptor s[4:7], q-block s3
+    nxt = [S('s_add_u32 s80, s99, s100'), S('s_sub_u32 s81, s71, 1'), S('s_min_u32 s80, s80, s81')]
+    nxt += sc['decode_map']
+    nxt += [S('s_sub_u32 s77, s77, s76'), S(f's_mov_b32 s{S_NQB}, s87'),
+            S('s_mov_b32 s0, s78'), S('s_sub_u32 s1, s79, s78'), S('s_mov_b32 s2, s89')]
+    nxt += make_desc(S_NQD, 40, 76, 62, 54, 55, 77)
+    lanes_t = [V(f'v_and_b32 v16, 31, v{V_TID}', 16, [V_TID]), V(f'v_bfe_u32 v17, v{V_TID}, 5, 1', 17, [V_TID]),
+               V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
+    pb1 = [label('.Lblock')] + nxt + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + \
+        sc['state'] + lanes_t + \
+        sc['rows'] + [S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')]
+    qcopy = [Inst(f'v_accvgpr_write_b32 a{A_Q[X] + r}, v{V_QN + 16 * xi + r}', 'accw',
+                  rd=[f'v{V_QN + 16 * xi + r}'], wr=[f'a{A_Q[X] + r}'])
+             for xi, X in enumerate(BLOCKS) for r in range(16)] + [raw('s_branch .Lqdone')]
+    qload = [label('.Lqload')] + sc['qload']
+    # next Q lane offsets (the 'rows' section's Q part with the next q-block's row base), then its loads
+    pf = [S(f's_lshl_b32 s93, s{S_WAVE}, 6'), S(f's_lshl_b32 s90, s{S_NQB}, 8'), S('s_add_u32 s93, s93, s90')]
+    for xi, (X, xo) in enumerate((('A', 0), ('B', 32))):
+        pf += [V('v_add_u32 v39, s93, v16', 39, [16])] + ([V(f'v_add_u32 v39, {xo}, v39', 39, [39])] if xo else [])
+        for ks in range(NKS):
+            o = V_QNOFF + 4 * xi + ks
+            pf += [V(f'v_add_u32 v40, {2 * ks}, v17', 40, [17]), V('v_lshlrev_b32 v41, 3, v40', 41, [40]),
+                   V('v_cmp_gt_u32 vcc, s74, v41', 'vcc', [41]),
+                   V('v_mul_lo_u32 v42, v39, s62', 42, [39]), V('v_lshl_add_u32 v42, v40, 4, v42', 42, [40, 42]),
+                   Inst(f'v_cndmask_b32 v{o}, v31, v42, vcc', 'valu', rd=['v31', 'v42', 'vcc'], wr=[f'v{o}'])]
+    for xi, X in enumerate(BLOCKS):
+        for ks in range(NKS):
+            q, o = V_QN + 16 * xi + 4 * ks, V_QNOFF + 4 * xi + ks
+            pf.append(Inst(f'buffer_load_dwordx4 {vs(q, 4)}, v{o}, s[{S_NQD}:{S_NQD + 3}], 0 offen', 'vload', 8,
+                           rd=[f'v{o}'], wr=rv(q, 4)))
+    pf.append(S('s_mov_b32 s101, 1'))
+    # tail start (PERSIST_KV): nt - 4 when nt % 4 == 0 and a next block exists, else never (-1)
+    pf += [S(f's_sub_u32 s{S_TAIL}, s{S_NT}, 4'), S(f's_and_b32 s96, s{S_NT}, 3'), S('s_cmp_lg_u32 s96, 0'),
+           S(f's_cselect_b32 s{S_TAIL}, -1, s{S_TAIL}'), S(f's_cmp_lt_u32 s{S_NT}, 4'),
+           S(f's_cselect_b32 s{S_TAIL}, -1, s{S_TAIL}'), S(f's_add_u32 s96, s{S_L}, s{S_G}'), S('s_cmp_ge_u32 s96, s71'),
+           S(f's_cselect_b32 s{S_TAIL}, -1, s{S_TAIL}')]
+    if not PERSIST_KV:
+        pf.append(S(f's_mov_b32 s{S_TAIL}, -1'))
+    nq = len(BLOCKS) * NKS
+
+    def start_with_wait(n):
+        st = [copy.copy(x) for x in sc['start']]
+        i = next(k for k, x in enumerate(st) if x.txt.startswith('s_waitcnt vmcnt('))
+        st[i] = raw(f's_waitcnt vmcnt({n})')
+        return st
+    # the first wait waits for Q, K0, K1, V0: younger are K2 V1 K3 V2 (8 pieces) and the next Q's loads
+    pb2 = [label('.Lqdone'), S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + sc['dma'] + pf + \
+        sc['zero'] + start_with_wait(4 * (DIST - 1) + nq)
+    # K0..K3 / V0..V2 came from the previous block's tail: the descriptor sets only walk as the
+    # prologue's DMAs would have; younger than K0 K1 V0 are the tail's last 8 pieces, this
+    # block's 2 x 5 O / LSE stores per wave and the next Q's loads
+    walk = g._dma('K', 2, walk_only=True) + g._dma('K', 3, walk_only=True) + g._dma('V', 2, walk_only=True)
+    pb2k = [label('.Lkvpf')] + walk + [copy.copy(x) for x in pf] + [copy.copy(x) for x in sc['zero']] + \
+        start_with_wait(4 * (DIST - 1) + N_STORES + nq) + [raw('s_branch .Lloop')]
+    return pro_a, pb1, qcopy, qload, pb2, pb2k
+
+
+N_STORES = 10         # LSE + O stores per wave of the 4-wave D = 64 epilogue (2 x (1 + 4))
+PERSIST_KV = True     # persistent form: the tail streams the next block's K0..K3 / V0..V2
+
+
+def tail_desc():
+    """The next block's K / V descriptor sets (tile 0 and tile 1 of its sequence) from s0 = its first
+    key row, s1 = seqlen_k, s2 = head (make_desc + the odd-tile sets of the prologue); temps s3, s29,
+    s31 (unused by the loop)."""
+    out = []
+    for kind, ptr, rs, hs in (('K', 42, 63, 56), ('V', 44, 64, 58)):
+        d0, d1 = S_NXD[kind]
+        out += [S(f's_mul_i32 s3, s0, s{rs}'), S(f's_mul_hi_u32 s29, s0, s{rs}'),
+                S(f's_add_u32 s{d0}, s{ptr}, s3'), S(f's_addc_u32 s{d0 + 1}, s{ptr + 1}, s29'),
+                S(f's_mul_i32 s3, s2, s{hs}'), S(f's_mul_hi_u32 s29, s2, s{hs}'), S(f's_mul_i32 s31, s2, s{hs + 1}'),
+                S('s_add_u32 s29, s29, s31'),
+                S(f's_add_u32 s{d0}, s{d0}, s3'), S(f's_addc_u32 s{d0 + 1}, s{d0 + 1}, s29'),
+                S(f's_mul_i32 s{d0 + 2}, s1, s{rs}'), S(f's_mov_b32 s{d0 + 3}, 0x00020000'),
+                S(f's_lshl_b32 s3, s{rs}, 6'),
+                S(f's_add_u32 s{d1}, s{d0}, s3'), S(f's_addc_u32 s{d1 + 1}, s{d0 + 1}, 0'),
+                S(f's_sub_u32 s{d1 + 2}, s{d0 + 2}, s3'), S(f's_cselect_b32 s{d1 + 2}, 0, s{d1 + 2}'),
+                S(f's_mov_b32 s{d1 + 3}, s{d0 + 3}')]
+    return out
 
 
 def dump_block(regs):
@@ -1414,7 +1596,7 @@ def stamp_exit():
         return []
     b = STAMP_V
     return stamp(b + 4) + [
-        raw(f's_load_dwordx2 s[98:99], s[0:1], {KARG_BYTES:#x}'), raw('s_waitcnt lgkmcnt(0)'),
+        raw(f's_load_dwordx2 s[98:99], s[0:1], {KARG_BYTES - 8:#x}'), raw('s_waitcnt lgkmcnt(0)'),
         raw(f'v_mov_b32 v{b + 11}, s{S_WAVE}'), raw('s_mov_b64 exec, 1'),
         raw(f'v_mov_b32 v{b + 14}, 1'), raw(f'v_mov_b32 v{b + 15}, 0'),
         raw(f'global_atomic_add v{b + 14}, v{b + 15}, v{b + 14}, s[98:99] sc0'), raw('s_waitcnt vmcnt(0)'),
@@ -1468,13 +1650,20 @@ def last_tile(g, t, rescue):
     else:
         b += [mark()] + place(g.pv_sum('B', t)[0], g.epilogue('A'))
         b += [mark()] + g.epilogue('B')
-    b += [raw('s_waitcnt vmcnt(0)')] + stamp_exit() + [raw('s_endpgm')]
+    if PERSIST:
+        b.append(raw('s_branch .Lseam'))
+    else:
+        b += [raw('s_waitcnt vmcnt(0)')] + stamp_exit() + [raw('s_endpgm')]
     return b
 
 
 def build(g):
     rescue = []
-    pro = stamp_entry() + prologue(g)
+    if PERSIST:
+        pro_a, pb1, qcopy, qload, pb2, pb2k = prologue_persist(g)
+        pro = pro_a + pb1 + qload + pb2       # (only for the DUMP hook below)
+    else:
+        pro = stamp_entry() + prologue(g)
     if DUMP and DUMP[0] == 'pro':
         pro += dump_block(DUMP[1])
     tiles = []
@@ -1483,6 +1672,8 @@ def build(g):
         if t == 0:
             blk.append(raw('.p2align 6'))
             blk.append(label('.Lloop'))
+        if PERSIST and t == 0:
+            blk += [S(f's_cmp_eq_u32 s{S_J}, s{S_TAIL}'), raw('s_cbranch_scc1 .Ltail')]
         blk += [S(f's_cmp_ge_u32 s{S_J}, s{S_MSTART}'), raw(f's_cbranch_scc1 .Lmask{t}')]
         if NWAVES == 8:
             blk += g.phase_w8(t, rescue=rescue)
@@ -1502,23 +1693,50 @@ def build(g):
     masks = [masked_tile(g, t, rescue) for t in range(U)]
     lasts = [last_tile(g, t, rescue) for t in range(U)]
     empty = [label('.Lempty')] + sum(([mark()] + g.epilogue(X) for X in BLOCKS), []) + \
-            [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
+            ([raw('s_branch .Lseam')] if PERSIST else [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')])
     end = [label('.Lend'), raw('s_endpgm')]
+    if PERSIST:
+        # .Lend (q-block past its sequence: nothing prefetched) and .Lseam (after a block): next block
+        end = [label('.Lend'), S(f's_mov_b32 s{S_QPF}, 0'), label('.Lseam'),
+               S(f's_add_u32 s{S_L}, s{S_L}, s{S_G}'), S(f's_cmp_ge_u32 s{S_L}, s71'), raw('s_cbranch_scc1 .Ldone'),
+               raw('s_barrier'), raw('s_branch .Lblock')]
+        done = [label('.Ldone'), raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
+        # a block past its sequence: the previous tail's DMAs must land before this slot reuse
+        end.insert(1, raw('s_waitcnt vmcnt(0)'))
+        tail = tail_blocks(g, rescue)
     # control-flow paths for the hazard pass
     paths = []
     def seq(blks):
         return sum((refs(b) for b in blks), [])
-    paths.append(lambda: refs(pro) + seq(tiles) + seq(tiles))
-    for t in range(U):
-        # main loop -> masked loop entered at position t -> a full masked round
-        paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
-        # masked loop -> last tile at position t
-        paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(masks) + seq(masks[:t]) + refs(lasts[t]))
-    paths.append(lambda: refs(pro) + refs(empty))
+    if PERSIST:
+        first = lambda: refs(pro_a) + refs(pb1) + refs(qload) + refs(pb2)
+        nxt = lambda: refs(end) + refs(pb1) + refs(qcopy) + refs(pb2)
+        lend = next(i for i, x in enumerate(pb1) if x.txt.endswith('.Lend'))
+        paths.append(lambda: first() + seq(tiles) + seq(tiles))
+        for t in range(U):
+            paths.append(lambda t=t: first() + seq(tiles) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
+            paths.append(lambda t=t: first() + seq(tiles) + seq(masks) + seq(masks[:t]) + refs(lasts[t]) + nxt() +
+                         seq(tiles))
+        paths.append(lambda: first() + refs(empty) + nxt() + seq(tiles))
+        paths.append(lambda: refs(pro_a) + [(pb1, k) for k in range(lend + 1)] + refs(end) + refs(pb1) + refs(qload) +
+                     refs(pb2) + seq(tiles))
+        itail = next(i for i, x in enumerate(tiles[0]) if x.txt.endswith('.Ltail'))
+        ikv = next(i for i, x in enumerate(pb2) if x.txt.endswith('.Lkvpf'))
+        for_tail = lambda: first() + seq(tiles) + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
+        paths.append(lambda: for_tail() + nxt_from_tail() + seq(tiles) + seq(tiles))
+        nxt_from_tail = lambda: refs(end) + refs(pb1) + refs(qcopy) + [(pb2, k) for k in range(ikv + 1)] + refs(pb2k)
+    else:
+        paths.append(lambda: refs(pro) + seq(tiles) + seq(tiles))
+        for t in range(U):
+            # main loop -> masked loop entered at position t -> a full masked round
+            paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
+            # masked loop -> last tile at position t
+            paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(masks) + seq(masks[:t]) + refs(lasts[t]))
+        paths.append(lambda: refs(pro) + refs(empty))
     # rescale blocks entered from their branch: the 40 instructions before it, the block, the rest
     def resc_path(rb):
         ret = rb[-1].txt.split()[-1]
-        for blk in tiles + masks + lasts:
+        for blk in tiles + masks + lasts + ([tail] if PERSIST else []):
             for i, x in enumerate(blk):
                 if x.kind == 'br' and x.txt.endswith(f'{ret}:'):
                     lo = max(0, i - 40)
@@ -1526,6 +1744,9 @@ def build(g):
         raise RuntimeError('rescale return not found')
     for rb in rescue:
         paths.append(lambda rb=rb: resc_path(rb))
+    if PERSIST:
+        n = fix_paths(paths)
+        return [pro_a, pb1, qcopy, qload, pb2] + tiles + masks + lasts + [empty, end, done, pb2k, tail] + rescue, n
     n = fix_paths(paths)
     blocks = [pro] + tiles + masks + lasts + [empty, end] + rescue
     return blocks, n
@@ -1604,6 +1825,7 @@ def main():
     ap.add_argument('--hd', type=int, default=64, choices=[64, 128], help='head-dim tile')
     ap.add_argument('--waves', type=int, default=4, choices=[4, 8], help='waves per workgroup (8: D = 64 only)')
     ap.add_argument('--prio4', type=int, default=None, help='8 waves: s_setprio 1 for waves 4-7')
+    ap.add_argument('--persist', type=int, default=0, help='persistent workgroups with next-Q prefetch (D = 64, 4 waves)')
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats', action='store_true')
     ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')
@@ -1646,6 +1868,7 @@ def main():
     global PRIO4
     if args.prio4 is not None:
         PRIO4 = bool(args.prio4)
+    set_persist(bool(args.persist))
     if MC_BANKS:
         NVGPR = max(NVGPR, V_MCB['B'] + 4)
     global KARG_BYTES

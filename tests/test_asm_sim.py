@@ -24,19 +24,21 @@ from oracle.attention_ref import attention_ref  # noqa: E402
 _TXT = {}
 
 
-def _kernel(dtype, hd=64, waves=4):
-    if (dtype, hd, waves) not in _TXT:
+def _kernel(dtype, hd=64, waves=4, persist=False):
+    if (dtype, hd, waves, persist) not in _TXT:
         gen_fwd.configure(hd, waves)
         try:
+            gen_fwd.set_persist(persist)
             g = gen_fwd.Gen(dtype)
             blocks, _ = gen_fwd.build(g)
-            _TXT[(dtype, hd, waves)] = gen_fwd.emit(g, blocks)
+            _TXT[(dtype, hd, waves, persist)] = gen_fwd.emit(g, blocks)
         finally:
             gen_fwd.configure(64)
-    return _TXT[(dtype, hd, waves)]
+    return _TXT[(dtype, hd, waves, persist)]
 
 
-def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4):
+def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4, grid=None):
+    """grid: the persistent form's workgroup count (each walks blocks L, L + grid, ...)."""
     rng = np.random.default_rng(seed)
     cv = asm_sim.bf16_bits if dtype == "bf16" else asm_sim.f16_bits
     B, tq, tk = len(lens_q), sum(lens_q), sum(lens_k)
@@ -65,8 +67,11 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4)
                        H * D * 2, H * D * 2, H * D * 2, H * D * 2, H, lse_stride * 4, c, np.float32(8.0 / c),
                        nqb, nqb * H * B, mg(nqb), mg(H), D, H * B, int(causal), mg(H * B),
                        per, mg(per) if per else 0, grp, mg(grp) if grp else 0)
+    if grid:
+        karg += struct.pack("<2I", grid, 0)
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
-    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64, waves), dtype).run((nqb, H, B), pa, mem)
+    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64, waves, bool(grid)), dtype).run(
+        (grid, 1, 1) if grid else (nqb, H, B), pa, mem)
     o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
     lse = mem.get(pl).view(np.float32).reshape(B, H, lse_stride)
     to = lambda x: torch.from_numpy(asm_sim.from16(x.astype(np.uint32), dtype))
@@ -177,3 +182,17 @@ def test_asm_forward_w8_in_simulator(lens_q, lens_k, causal, dtype):
 def test_asm_forward_w8_rescale_path_in_simulator():
     """The 8-wave form's rescale block runs after the phase's P.V MFMAs into the same O."""
     _run([70], [300], 1, 64, "bf16", scale=3.0, waves=8)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("lens_q,lens_k,H,D,grid", [
+    ([130], [200], 3, 64, 1),             # one workgroup walks all 3 blocks (next-Q prefetch each time)
+    ([257, 40], [33, 190], 2, 64, 3),     # var-len, 3 workgroups over 8 blocks: empty q-blocks (.Lend)
+    ([70, 300], [700, 0], 2, 48, 2),      # 11 tiles, empty key set, head_dim < 64 (masked Q chunks)
+    ([300, 200], [512, 256], 2, 64, 1),   # nt = 8 and 4: the tail streams the next block's K/V tiles
+    ([300, 100], [512, 320], 2, 64, 3),   # tails into a next block with nt % 4 != 0, and into an empty q-block
+])
+def test_asm_forward_persistent_in_simulator(lens_q, lens_k, H, D, grid, dtype):
+    """The persistent form (one workgroup walks blocks L, L + grid, ...; the next block's Q is
+    prefetched into spare VGPRs and copied at the seam; a block past its sequence skips to the next)."""
+    _run(lens_q, lens_k, H, D, dtype, grid=grid)

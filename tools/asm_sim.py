@@ -338,6 +338,9 @@ class Sim:
         elif op == 's_cmp_eq_u32':
             w.scc = self.sread(w, a[0]) == x
             return
+        elif op == 's_cmp_lt_u32':
+            w.scc = self.sread(w, a[0]) < x
+            return
         elif op == 's_cmp_lg_u32':
             w.scc = self.sread(w, a[0]) != x
             return

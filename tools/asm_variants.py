@@ -34,7 +34,8 @@ def build(spec, out_dir):
     txt = open(s).read()
     name = txt.split(".globl ")[1].split()[0]
     threads = int(txt.split(".max_flat_workgroup_size: ")[1].split()[0])
-    return open(s[:-2] + ".hsaco", "rb").read(), name, threads
+    persist = int(txt.split(".kernarg_segment_size: ")[1].split()[0]) == 176
+    return open(s[:-2] + ".hsaco", "rb").read(), name, (threads, persist)
 
 
 def main():
@@ -75,6 +76,12 @@ def main():
     kbuf = ctypes.create_string_buffer(kb, len(kb))
     size = ctypes.c_size_t(len(kb))
     extra = (ctypes.c_void_p * 5)(1, ctypes.addressof(kbuf), 2, ctypes.addressof(size), 3)
+    # persistent kernels: the grid size (one workgroup per CU) in the 8 bytes after the block
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count // 8 * 8
+    kbp = kb + struct.pack("<2I", ncu, 0)
+    kbufp = ctypes.create_string_buffer(kbp, len(kbp))
+    sizep = ctypes.c_size_t(len(kbp))
+    extrap = (ctypes.c_void_p * 5)(1, ctypes.addressof(kbufp), 2, ctypes.addressof(sizep), 3)
     fns = {}
     keep = []
     threads = {}
@@ -89,7 +96,11 @@ def main():
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def launch(fn):
-        rc = hip.hipModuleLaunchKernel(fn, nqb, H, B, threads[fn.value], 1, 1, 0, stream, None, extra)
+        nthr, persist = threads[fn.value]
+        if persist:
+            rc = hip.hipModuleLaunchKernel(fn, min(ncu, nqb * H * B), 1, 1, nthr, 1, 1, 0, stream, None, extrap)
+        else:
+            rc = hip.hipModuleLaunchKernel(fn, nqb, H, B, nthr, 1, 1, 0, stream, None, extra)
         assert rc == 0
 
     flops = 4.0 * B * H * S * S * D
