@@ -5,7 +5,8 @@
 Workload (BASELINE.json north star): B=8, H=12, S=2048, D=64, bf16, non-causal, forward,
 unpadded layout (B*S, H, D), synthetic N(0,1) inputs resident in HBM. One step = one forward
 pass over the batch through the drop-in interface (flash_attn_unpadded_func -> compiled binding
--> C ABI -> the hand-scheduled gfx950 assembly forward fa_fwd_d64_bf16_asm, csrc/asm/gen_fwd.py).
+-> C ABI -> the hand-scheduled gfx950 assembly forward in its persistent form fa_fwd_d64p_bf16_asm,
+csrc/asm/gen_fwd.py --persist 1: one workgroup per CU walks three of the 768 blocks).
 Multi-GPU: one process per GPU (torchrun), independent replicas (attention is per-sample, no
 collective); value = total FLOPs of all ranks / max time.
 
@@ -206,7 +207,7 @@ def main():
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": read_traffic(),
                 "measured_mfma_ceiling": MFMA_CEILING_RANDOM_TFLOPS,
                 "frac_of_measured_ceiling": round(achieved / MFMA_CEILING_RANDOM_TFLOPS, 4),
-                "kernel": "fa_fwd_d64_bf16_asm (csrc/asm/gen_fwd.py)", "avg_kernel_ms": round(avg_ms, 4),
+                "kernel": "fa_fwd_d64p_bf16_asm (csrc/asm/gen_fwd.py --persist 1)", "avg_kernel_ms": round(avg_ms, 4),
                 "flops_per_launch": flops, "algorithmic_bytes_per_launch": fwd_bytes(B, H, S, S, D)}
 
     extra = {}

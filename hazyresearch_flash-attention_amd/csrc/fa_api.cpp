@@ -144,8 +144,8 @@ int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
     if ((int64_t)a->max_seqlen_q * a->q_row_stride * 2 >= lim || (int64_t)a->max_seqlen_k * a->k_row_stride * 2 >= lim ||
         (int64_t)a->max_seqlen_k * a->v_row_stride * 2 >= lim)
         return fail(FA_ERR_UNSUPPORTED, "fa_fwd: a sequence spans more than 2 GiB (seqlen * row_stride)");
-    if (a->impl < FA_IMPL_AUTO || a->impl > FA_IMPL_ASM8)
-        return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: impl must be one of FA_IMPL_AUTO / HIP / ASM4 / ASM8");
+    if (a->impl < FA_IMPL_AUTO || a->impl > FA_IMPL_ASM4P)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: impl must be one of FA_IMPL_AUTO / HIP / ASM4 / ASM8 / ASM4P");
     if (a->max_seqlen_q == 0) return FA_OK;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;

@@ -30,6 +30,10 @@ extern const unsigned char fa_asm_fwd_d64w8_bf16[];
 extern const unsigned long fa_asm_fwd_d64w8_bf16_size;
 extern const unsigned char fa_asm_fwd_d64w8_f16[];
 extern const unsigned long fa_asm_fwd_d64w8_f16_size;
+extern const unsigned char fa_asm_fwd_d64p_bf16[];
+extern const unsigned long fa_asm_fwd_d64p_bf16_size;
+extern const unsigned char fa_asm_fwd_d64p_f16[];
+extern const unsigned long fa_asm_fwd_d64p_f16_size;
 }
 
 namespace fa {
@@ -57,8 +61,11 @@ struct FaAsmFwdArgs {
     // causal XCD groups (fa_common.h xcd_grouped): each XCD runs its nbh / 8 heads in groups of G,
     // heaviest q-block first across a group; per = G nqb (0: the global heaviest-first order)
     uint32_t per, magic_per, group, magic_group;
+    // persistent form only (gen_fwd.py --persist, KARG_BYTES 176): workgroups in the 1-D grid; each
+    // walks logical blocks L = blockIdx.x + r * persist_grid
+    uint32_t persist_grid, pad;
 };
-static_assert(sizeof(FaAsmFwdArgs) == 168, "FaAsmFwdArgs layout (gen_fwd.py KARG_BYTES)");
+static_assert(sizeof(FaAsmFwdArgs) == 176, "FaAsmFwdArgs layout (gen_fwd.py KARG_BYTES)");
 static_assert(offsetof(FaAsmFwdArgs, q_rs) == 88 && offsetof(FaAsmFwdArgs, c) == 112 &&
               offsetof(FaAsmFwdArgs, magic_nqb) == 128 && offsetof(FaAsmFwdArgs, head_dim) == 136 &&
                   offsetof(FaAsmFwdArgs, causal) == 144,
@@ -70,8 +77,9 @@ constexpr int kRows = 256;            // query rows per workgroup
 constexpr int kMaxDev = 64;
 constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
 
-// kernels: [form (0: D=64, 1: D=128, 2: D=64 two waves per SIMD) * 2 + dtype (0: bf16, 1: f16)]
-constexpr int kNumFns = 6;
+// kernels: [form (0: D=64, 1: D=128, 2: D=64 two waves per SIMD, 3: D=64 persistent) * 2 + dtype
+// (0: bf16, 1: f16)]
+constexpr int kNumFns = 8;
 struct DevFns {
     hipModule_t mod[kNumFns] = {};
     hipFunction_t fn[kNumFns] = {};
@@ -88,11 +96,14 @@ hipError_t get_function(int dtype, int form, hipFunction_t *out) {
     std::lock_guard<std::mutex> lk(g_mu);
     DevFns &d = g_fns[dev];
     if (!d.fn[k]) {
-        static const void *const imgs[kNumFns] = {fa_asm_fwd_d64_bf16, fa_asm_fwd_d64_f16, fa_asm_fwd_d128_bf16,
-                                                  fa_asm_fwd_d128_f16, fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16};
-        static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm", "fa_fwd_d64_f16_asm",
-                                                   "fa_fwd_d128_bf16_asm", "fa_fwd_d128_f16_asm",
-                                                   "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm"};
+        static const void *const imgs[kNumFns] = {fa_asm_fwd_d64_bf16,   fa_asm_fwd_d64_f16,
+                                                  fa_asm_fwd_d128_bf16,  fa_asm_fwd_d128_f16,
+                                                  fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16,
+                                                  fa_asm_fwd_d64p_bf16,  fa_asm_fwd_d64p_f16};
+        static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
+                                                   "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
+                                                   "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
+                                                   "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm"};
         const void *img = imgs[k];
         const char *name = names[k];
         e = hipModuleLoadData(&d.mod[k], img);
@@ -135,16 +146,40 @@ bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
 }
 
 // The two-waves-per-SIMD form (8-wave workgroups, one 32-row block per wave) serves head_dim == 64
-// only (its Q loads and O stores address whole rows from one base).
-static bool use_w8(const FaFwdArgs &a) {
-    if (a.head_dim != 64 || a.impl == FA_IMPL_ASM4) return false;
-    return a.impl == FA_IMPL_ASM8;
+// only (its Q loads and O stores address whole rows from one base); measured even with the
+// one-wave form, it runs only when forced.
+static bool use_w8(const FaFwdArgs &a) { return a.head_dim == 64 && a.impl == FA_IMPL_ASM8; }
+
+// CUs of the current device rounded down to whole XCD rounds (8): the persistent grid, so that
+// workgroup P walks L = P, P + G, ... in the XCD-aware block order of the one-block launch.
+static int persist_grid() {
+    static int cache[kMaxDev] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cache[dev] = n / 8 * 8;
+    }
+    return cache[dev];
+}
+
+// The persistent form (D=64 tile, non-causal): by default when the grid has more blocks than
+// CUs (measured -1.8 % at the north star's 3 rounds, -3.4 % at 6); FA_IMPL_ASM4P forces it.
+static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
+    if (a.head_dim > 64 || a.is_causal || a.impl == FA_IMPL_ASM4 || a.impl == FA_IMPL_ASM8) return 0;
+    const int g = persist_grid();
+    if (g < 8) return 0;
+    if (a.impl == FA_IMPL_ASM4P) return (int)(nwg < (uint32_t)g ? nwg : (uint32_t)g);
+    return nwg > (uint32_t)g ? g : 0;
 }
 
 hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
     hipFunction_t fn = nullptr;
     const bool w8 = use_w8(a);
-    hipError_t e = get_function(a.dtype, w8 ? 2 : (a.head_dim > 64 ? 1 : 0), &fn);
+    const uint32_t nqb0 = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
+    const int pgrid = w8 ? 0 : persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
+    hipError_t e = get_function(a.dtype, w8 ? 2 : pgrid ? 3 : (a.head_dim > 64 ? 1 : 0), &fn);
     if (e != hipSuccess) return e;
     FaAsmFwdArgs k;
     std::memset(&k, 0, sizeof(k));
@@ -188,10 +223,15 @@ hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
         k.group = g;
         k.magic_group = magic_half(g);
     }
-    size_t size = sizeof(k);
+    k.persist_grid = (uint32_t)pgrid;
+    // the one-block forms take the 168-byte block (their kernarg segment size)
+    size_t size = pgrid ? sizeof(k) : offsetof(FaAsmFwdArgs, persist_grid);
     void *config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
-    e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, w8 ? 2 * kRows : kRows, 1, 1, 0, stream,
-                              nullptr, config);
+    if (pgrid)
+        e = hipModuleLaunchKernel(fn, (unsigned)pgrid, 1, 1, kRows, 1, 1, 0, stream, nullptr, config);
+    else
+        e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, w8 ? 2 * kRows : kRows, 1, 1, 0,
+                                  stream, nullptr, config);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -101,15 +101,16 @@ typedef struct FaFwdArgs {
     int64_t rot_stride;
     /* Kernel family (FA_IMPL_*). FA_IMPL_AUTO picks the fastest kernel for the shape: the
      * hand-scheduled assembly forward for head_dim in (32, 64] or 128, fp16/bf16, no dropout,
-     * dense, no fused rotary (at head_dim == 64 its two-waves-per-SIMD form where that measured
-     * faster); the HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels; FA_IMPL_ASM4 /
-     * FA_IMPL_ASM8 force the one- / two-waves-per-SIMD assembly form where the shape is eligible
-     * (tests compare them; results agree within fp32 rounding of the row sums). */
+     * dense, no fused rotary (non-causal head_dim in (32, 64] grids larger than the CU count take
+     * its persistent form); the HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels;
+     * FA_IMPL_ASM4 / FA_IMPL_ASM8 / FA_IMPL_ASM4P force the one-wave-per-SIMD, the
+     * two-waves-per-SIMD and the persistent one-wave-per-SIMD assembly form where the shape is
+     * eligible (tests compare them; results agree within fp32 rounding of the row sums). */
     int32_t impl;
     int32_t reserved;         /* 0 */
 } FaFwdArgs;
 
-enum { FA_IMPL_AUTO = 0, FA_IMPL_HIP = 1, FA_IMPL_ASM4 = 2, FA_IMPL_ASM8 = 3 };
+enum { FA_IMPL_AUTO = 0, FA_IMPL_HIP = 1, FA_IMPL_ASM4 = 2, FA_IMPL_ASM8 = 3, FA_IMPL_ASM4P = 4 };
 
 /* Backward arguments. Mirrors the bwd call made by flash_attn_interface.py:31-33:
  * bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_q, cu_k, max_q, max_k, p, scale,
