@@ -4,6 +4,10 @@ its final stores, plus its CU (HW_ID / XCC_ID). Reports, per workgroup, prologue
 durations and the gap between consecutive workgroups on one CU (dispatch latency).
 
     python tools/asm_wg_timeline.py [--shape B,H,Sq,Sk] [--causal]
+
+Status: its first hardware run (round 3) faulted with an illegal address: the stamps probe read its
+buffer pointer 8 bytes past the argument block (KARG_BYTES after the += 8). gen_fwd.py now reads it at
+KARG_BYTES - 8; the fixed probe has not been run on hardware since. Run it alone, under a short timeout.
 """
 import argparse
 import ctypes
