@@ -1436,10 +1436,15 @@ def tail_blocks(g, rescue):
 def set_persist(on):
     """Persistent form on/off (D = 64, 4 waves): 8 more kernel-argument bytes (grid size at 168),
     registers up to V_TID."""
-    global PERSIST, KARG_BYTES, NVGPR
+    global PERSIST, KARG_BYTES, NVGPR, V_TID, PERSIST_Q, N_STORES
     if on:
-        assert D == 64 and NWAVES == 4 and not MC_BANKS
-        NVGPR = max(NVGPR, NVGPR_PERSIST)
+        assert NWAVES == 4 and not MC_BANKS
+        # D = 128: Q, row sums and the indicator fill the VGPRs (no room for the next Q): K/V tail
+        # only, the workitem id in the last free VGPR
+        PERSIST_Q = D == 64
+        V_TID = 208 if PERSIST_Q else 251
+        NVGPR = max(NVGPR, NVGPR_PERSIST if PERSIST_Q else V_TID + 1)
+        N_STORES = len(BLOCKS) * (1 + 2 * NDT)
         KARG_BYTES = 176
     else:
         KARG_BYTES = 168
@@ -1464,14 +1469,16 @@ def prologue_persist(g):
                V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
     pb1 = [label('.Lblock')] + nxt + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + \
         sc['state'] + lanes_t + \
-        sc['rows'] + [S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')]
+        sc['rows'] + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
     qcopy = [Inst(f'v_accvgpr_write_b32 a{A_Q[X] + r}, v{V_QN + 16 * xi + r}', 'accw',
                   rd=[f'v{V_QN + 16 * xi + r}'], wr=[f'a{A_Q[X] + r}'])
              for xi, X in enumerate(BLOCKS) for r in range(16)] + [raw('s_branch .Lqdone')]
+    if not PERSIST_Q:
+        qcopy = []
     qload = [label('.Lqload')] + sc['qload']
     # next Q lane offsets (the 'rows' section's Q part with the next q-block's row base), then its loads
     pf = [S(f's_lshl_b32 s93, s{S_WAVE}, 6'), S(f's_lshl_b32 s90, s{S_NQB}, 8'), S('s_add_u32 s93, s93, s90')]
-    for xi, (X, xo) in enumerate((('A', 0), ('B', 32))):
+    for xi, (X, xo) in enumerate((('A', 0), ('B', 32)) if PERSIST_Q else ()):
         pf += [V('v_add_u32 v39, s93, v16', 39, [16])] + ([V(f'v_add_u32 v39, {xo}, v39', 39, [39])] if xo else [])
         for ks in range(NKS):
             o = V_QNOFF + 4 * xi + ks
@@ -1479,7 +1486,7 @@ def prologue_persist(g):
                    V('v_cmp_gt_u32 vcc, s74, v41', 'vcc', [41]),
                    V('v_mul_lo_u32 v42, v39, s62', 42, [39]), V('v_lshl_add_u32 v42, v40, 4, v42', 42, [40, 42]),
                    Inst(f'v_cndmask_b32 v{o}, v31, v42, vcc', 'valu', rd=['v31', 'v42', 'vcc'], wr=[f'v{o}'])]
-    for xi, X in enumerate(BLOCKS):
+    for xi, X in enumerate(BLOCKS if PERSIST_Q else ''):
         for ks in range(NKS):
             q, o = V_QN + 16 * xi + 4 * ks, V_QNOFF + 4 * xi + ks
             pf.append(Inst(f'buffer_load_dwordx4 {vs(q, 4)}, v{o}, s[{S_NQD}:{S_NQD + 3}], 0 offen', 'vload', 8,
@@ -1492,7 +1499,7 @@ def prologue_persist(g):
            S(f's_cselect_b32 s{S_TAIL}, -1, s{S_TAIL}')]
     if not PERSIST_KV:
         pf.append(S(f's_mov_b32 s{S_TAIL}, -1'))
-    nq = len(BLOCKS) * NKS
+    nq = len(BLOCKS) * NKS if PERSIST_Q else 0
 
     def start_with_wait(n):
         st = [copy.copy(x) for x in sc['start']]
@@ -1507,11 +1514,12 @@ def prologue_persist(g):
     # block's 2 x 5 O / LSE stores per wave and the next Q's loads
     walk = g._dma('K', 2, walk_only=True) + g._dma('K', 3, walk_only=True) + g._dma('V', 2, walk_only=True)
     pb2k = [label('.Lkvpf')] + walk + [copy.copy(x) for x in pf] + [copy.copy(x) for x in sc['zero']] + \
-        start_with_wait(4 * (DIST - 1) + N_STORES + nq) + [raw('s_branch .Lloop')]
+        start_with_wait(4 * NP + N_STORES + nq) + [raw('s_branch .Lloop')]
     return pro_a, pb1, qcopy, qload, pb2, pb2k
 
 
-N_STORES = 10         # LSE + O stores per wave of the 4-wave D = 64 epilogue (2 x (1 + 4))
+N_STORES = 10         # LSE + O stores per wave of the epilogue (D = 64: 2 x (1 + 4); set_persist)
+PERSIST_Q = True      # persistent form: next-block Q prefetch (D = 64 only)
 PERSIST_KV = True     # persistent form: the tail streams the next block's K0..K3 / V0..V2
 
 
@@ -1710,7 +1718,8 @@ def build(g):
         return sum((refs(b) for b in blks), [])
     if PERSIST:
         first = lambda: refs(pro_a) + refs(pb1) + refs(qload) + refs(pb2)
-        nxt = lambda: refs(end) + refs(pb1) + refs(qcopy) + refs(pb2)
+        qsel = qcopy if PERSIST_Q else qload
+        nxt = lambda: refs(end) + refs(pb1) + refs(qsel) + refs(pb2)
         lend = next(i for i, x in enumerate(pb1) if x.txt.endswith('.Lend'))
         paths.append(lambda: first() + seq(tiles) + seq(tiles))
         for t in range(U):
@@ -1724,7 +1733,7 @@ def build(g):
         ikv = next(i for i, x in enumerate(pb2) if x.txt.endswith('.Lkvpf'))
         for_tail = lambda: first() + seq(tiles) + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
         paths.append(lambda: for_tail() + nxt_from_tail() + seq(tiles) + seq(tiles))
-        nxt_from_tail = lambda: refs(end) + refs(pb1) + refs(qcopy) + [(pb2, k) for k in range(ikv + 1)] + refs(pb2k)
+        nxt_from_tail = lambda: refs(end) + refs(pb1) + refs(qsel) + [(pb2, k) for k in range(ikv + 1)] + refs(pb2k)
     else:
         paths.append(lambda: refs(pro) + seq(tiles) + seq(tiles))
         for t in range(U):
@@ -1825,7 +1834,7 @@ def main():
     ap.add_argument('--hd', type=int, default=64, choices=[64, 128], help='head-dim tile')
     ap.add_argument('--waves', type=int, default=4, choices=[4, 8], help='waves per workgroup (8: D = 64 only)')
     ap.add_argument('--prio4', type=int, default=None, help='8 waves: s_setprio 1 for waves 4-7')
-    ap.add_argument('--persist', type=int, default=0, help='persistent workgroups with next-Q prefetch (D = 64, 4 waves)')
+    ap.add_argument('--persist', type=int, default=0, help='persistent workgroups: next-block K/V tail (and next-Q prefetch at D = 64), 4 waves')
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats', action='store_true')
     ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')

@@ -34,6 +34,10 @@ extern const unsigned char fa_asm_fwd_d64p_bf16[];
 extern const unsigned long fa_asm_fwd_d64p_bf16_size;
 extern const unsigned char fa_asm_fwd_d64p_f16[];
 extern const unsigned long fa_asm_fwd_d64p_f16_size;
+extern const unsigned char fa_asm_fwd_d128p_bf16[];
+extern const unsigned long fa_asm_fwd_d128p_bf16_size;
+extern const unsigned char fa_asm_fwd_d128p_f16[];
+extern const unsigned long fa_asm_fwd_d128p_f16_size;
 }
 
 namespace fa {
@@ -77,9 +81,9 @@ constexpr int kRows = 256;            // query rows per workgroup
 constexpr int kMaxDev = 64;
 constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
 
-// kernels: [form (0: D=64, 1: D=128, 2: D=64 two waves per SIMD, 3: D=64 persistent) * 2 + dtype
-// (0: bf16, 1: f16)]
-constexpr int kNumFns = 8;
+// kernels: [form (0: D=64, 1: D=128, 2: D=64 two waves per SIMD, 3: D=64 persistent, 4: D=128
+// persistent) * 2 + dtype (0: bf16, 1: f16)]
+constexpr int kNumFns = 10;
 struct DevFns {
     hipModule_t mod[kNumFns] = {};
     hipFunction_t fn[kNumFns] = {};
@@ -99,11 +103,13 @@ hipError_t get_function(int dtype, int form, hipFunction_t *out) {
         static const void *const imgs[kNumFns] = {fa_asm_fwd_d64_bf16,   fa_asm_fwd_d64_f16,
                                                   fa_asm_fwd_d128_bf16,  fa_asm_fwd_d128_f16,
                                                   fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16,
-                                                  fa_asm_fwd_d64p_bf16,  fa_asm_fwd_d64p_f16};
+                                                  fa_asm_fwd_d64p_bf16,  fa_asm_fwd_d64p_f16,
+                                                  fa_asm_fwd_d128p_bf16, fa_asm_fwd_d128p_f16};
         static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
                                                    "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
                                                    "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
-                                                   "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm"};
+                                                   "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
+                                                   "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm"};
         const void *img = imgs[k];
         const char *name = names[k];
         e = hipModuleLoadData(&d.mod[k], img);
@@ -164,10 +170,11 @@ static int persist_grid() {
     return cache[dev];
 }
 
-// The persistent form (D=64 tile, non-causal): by default when the grid has more blocks than
-// CUs (measured -1.8 % at the north star's 3 rounds, -3.4 % at 6); FA_IMPL_ASM4P forces it.
+// The persistent form (D=64 and D=128 tiles, non-causal): by default when the grid has more blocks
+// than CUs (measured -1.8 % at the north star's 3 rounds, -3.4 % at 6; D=128 -1.6 % at 3 rounds,
+// even at 12); FA_IMPL_ASM4P forces it. Causal grids keep the dispatcher's dynamic balance.
 static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
-    if (a.head_dim > 64 || a.is_causal || a.impl == FA_IMPL_ASM4 || a.impl == FA_IMPL_ASM8) return 0;
+    if (a.is_causal || a.impl == FA_IMPL_ASM4 || a.impl == FA_IMPL_ASM8) return 0;
     const int g = persist_grid();
     if (g < 8) return 0;
     if (a.impl == FA_IMPL_ASM4P) return (int)(nwg < (uint32_t)g ? nwg : (uint32_t)g);
@@ -179,7 +186,8 @@ hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
     const bool w8 = use_w8(a);
     const uint32_t nqb0 = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
     const int pgrid = w8 ? 0 : persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
-    hipError_t e = get_function(a.dtype, w8 ? 2 : pgrid ? 3 : (a.head_dim > 64 ? 1 : 0), &fn);
+    const bool d128 = a.head_dim > 64;
+    hipError_t e = get_function(a.dtype, w8 ? 2 : pgrid ? (d128 ? 4 : 3) : (d128 ? 1 : 0), &fn);
     if (e != hipSuccess) return e;
     FaAsmFwdArgs k;
     std::memset(&k, 0, sizeof(k));

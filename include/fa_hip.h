@@ -101,7 +101,7 @@ typedef struct FaFwdArgs {
     int64_t rot_stride;
     /* Kernel family (FA_IMPL_*). FA_IMPL_AUTO picks the fastest kernel for the shape: the
      * hand-scheduled assembly forward for head_dim in (32, 64] or 128, fp16/bf16, no dropout,
-     * dense, no fused rotary (non-causal head_dim in (32, 64] grids larger than the CU count take
+     * dense, no fused rotary (non-causal grids with more blocks than CUs take
      * its persistent form); the HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels;
      * FA_IMPL_ASM4 / FA_IMPL_ASM8 / FA_IMPL_ASM4P force the one-wave-per-SIMD, the
      * two-waves-per-SIMD and the persistent one-wave-per-SIMD assembly form where the shape is

@@ -77,3 +77,12 @@ def test_asm_persistent_var_len_many_blocks():
     hip = _hip()
     with hip.force_impl(hip.FA_IMPL_ASM4P):
         run_case("separate", 40, 600, 1100, 8, 64, torch.bfloat16, False, 0.0, grad=False, seed=11)
+
+
+@pytest.mark.parametrize("form", ["ASM4", "ASM4P"])
+@pytest.mark.parametrize("seqlen_q,seqlen_k", [(257, 513), (1025, 1100), (2048, 2048)])
+def test_asm_form_forward_d128(form, seqlen_q, seqlen_k):
+    """The head_dim = 128 tile in its one-block and persistent forms (grids of 72-384 blocks)."""
+    hip = _hip()
+    with hip.force_impl(getattr(hip, f"FA_IMPL_{form}")):
+        run_case("separate", 6, seqlen_q, seqlen_k, 8, 128, torch.bfloat16, False, 0.0, grad=False, seed=seqlen_k)

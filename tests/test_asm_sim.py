@@ -151,8 +151,9 @@ def test_asm_forward_rescale_path_in_simulator():
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("hd,waves", [(64, 4), (128, 4), (64, 8)])
-def test_generated_kernel_assembles(dtype, hd, waves, tmp_path):
+@pytest.mark.parametrize("hd,waves,persist", [(64, 4, False), (128, 4, False), (64, 8, False), (64, 4, True),
+                                               (128, 4, True)])
+def test_generated_kernel_assembles(dtype, hd, waves, persist, tmp_path):
     """The simulator does not check encodings (register alignment, gfx950 operand forms): the
     product kernels must also assemble for gfx950, as build.py does."""
     import subprocess
@@ -160,7 +161,7 @@ def test_generated_kernel_assembles(dtype, hd, waves, tmp_path):
     if not os.path.exists(llvm):
         pytest.skip("no ROCm LLVM")
     s = tmp_path / "k.s"
-    s.write_text(_kernel(dtype, hd, waves))
+    s.write_text(_kernel(dtype, hd, waves, persist))
     r = subprocess.run([llvm, "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c", str(s),
                         "-o", str(tmp_path / "k.o")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -196,3 +197,12 @@ def test_asm_forward_persistent_in_simulator(lens_q, lens_k, H, D, grid, dtype):
     """The persistent form (one workgroup walks blocks L, L + grid, ...; the next block's Q is
     prefetched into spare VGPRs and copied at the seam; a block past its sequence skips to the next)."""
     _run(lens_q, lens_k, H, D, dtype, grid=grid)
+
+
+@pytest.mark.parametrize("lens_q,lens_k,H,grid", [
+    ([300, 200], [512, 256], 2, 1),       # nt = 8 and 4: the tail streams the next block's K/V tiles
+    ([300, 100], [512, 320], 2, 3),       # tails into a block with nt % 4 != 0 and into an empty q-block
+])
+def test_asm_forward_persistent_d128_in_simulator(lens_q, lens_k, H, grid):
+    """The persistent form at head_dim = 128 (K/V tail only: Q stays in VGPRs, no next-Q prefetch)."""
+    _run(lens_q, lens_k, H, 128, "bf16", grid=grid)

@@ -19,7 +19,7 @@ GEN = os.path.join(ROOT, "hazyresearch_flash-attention_amd", "csrc", "asm", "gen
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-def build(spec, out_dir):
+def build(spec, out_dir, hd=64):
     """spec: 'label:generator args' (e.g. 'vp1:--vp1 1 --probe noexp') or a bare probe switch."""
     if ":" in spec:
         tag, args = spec.split(":", 1)
@@ -27,7 +27,7 @@ def build(spec, out_dir):
     else:
         tag, extra = spec or "base", (["--probe", spec] if spec else [])
     s = os.path.join(out_dir, f"var_{tag}.s")
-    subprocess.check_call([sys.executable, GEN, "--out", s] + list(extra))
+    subprocess.check_call([sys.executable, GEN, "--out", s, "--hd", str(hd)] + list(extra))
     subprocess.check_call([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
                            s, "-o", s[:-2] + ".o"])
     subprocess.check_call([f"{LLVM}/ld.lld", "-shared", s[:-2] + ".o", "-o", s[:-2] + ".hsaco"])
@@ -43,16 +43,17 @@ def main():
     ap.add_argument("--shape", default="8,12,2048")
     ap.add_argument("--variants", default=",nomax,noexp,nofma,nocvt,nofill,nodma,nolds,nosum,nobar")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--hd", type=int, default=64, choices=[64, 128])
     ap.add_argument("--iters", type=int, default=50)
     args = ap.parse_args()
     out = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out, exist_ok=True)
     # ';'-separated 'label:generator args' specs, or ','-separated probe switches ('' = base)
     variants = args.variants.split(";") if ";" in args.variants else args.variants.split(",")
-    images = {v: build(v, out) for v in variants}
+    images = {v: build(v, out, args.hd) for v in variants}
     import torch
     B, H, S = (int(x) for x in args.shape.split(","))
-    D = 64
+    D = args.hd
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     q = torch.randn(B * S, H, D, generator=g).bfloat16().to(dev)
