@@ -11,6 +11,7 @@
 // rows past a sequence neither read nor written, LSE = m*scale + ln(sum) (-inf for no keys).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -159,15 +160,17 @@ static bool use_w8(const FaFwdArgs &a) { return a.head_dim == 64 && a.impl == FA
 // CUs of the current device rounded down to whole XCD rounds (8): the persistent grid, so that
 // workgroup P walks L = P, P + G, ... in the XCD-aware block order of the one-block launch.
 static int persist_grid() {
-    static int cache[kMaxDev] = {};
+    static std::atomic<int> cache[kMaxDev] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
-    if (!cache[dev]) {
+    int g = cache[dev].load(std::memory_order_relaxed);
+    if (!g) {
         int n = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-        cache[dev] = n / 8 * 8;
+        g = n / 8 * 8;
+        cache[dev].store(g, std::memory_order_relaxed);
     }
-    return cache[dev];
+    return g;
 }
 
 // The persistent form (D=64 and D=128 tiles, non-causal): by default when the grid has more blocks
