@@ -22,12 +22,27 @@ hipError_t launch_probs(const FaFwdArgs &a, const FaBlockMask &bm, hipStream_t s
     return a.dtype == FA_DTYPE_BF16 ? launch_probs_dt<Bf16>(a, bm, s) : launch_probs_dt<Fp16>(a, bm, s);
 }
 
-hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t s) {
-    dim3 grid((a.max_seqlen_q + 15) / 16, a.nheads, a.batch);
-    if (a.dtype == FA_DTYPE_BF16)
-        hipLaunchKernelGGL(fa_bwd_dot_kernel<Bf16>, grid, dim3(256), 0, s, a);
+template <typename T, int CPR>
+static void launch_dot(const FaBwdArgs &a, hipStream_t s) {
+    dim3 grid((a.max_seqlen_q + 256 / CPR - 1) / (256 / CPR), a.nheads, a.batch);
+    hipLaunchKernelGGL((fa_bwd_dot_kernel<T, CPR>), grid, dim3(256), 0, s, a);
+}
+
+template <typename T>
+static void launch_dot_t(const FaBwdArgs &a, hipStream_t s) {
+    if (a.head_dim <= 32)
+        launch_dot<T, 4>(a, s);
+    else if (a.head_dim <= 64)
+        launch_dot<T, 8>(a, s);
     else
-        hipLaunchKernelGGL(fa_bwd_dot_kernel<Fp16>, grid, dim3(256), 0, s, a);
+        launch_dot<T, 16>(a, s);
+}
+
+hipError_t launch_bwd_pre(const FaBwdArgs &a, hipStream_t s) {
+    if (a.dtype == FA_DTYPE_BF16)
+        launch_dot_t<Bf16>(a, s);
+    else
+        launch_dot_t<Fp16>(a, s);
     return hipGetLastError();
 }
 

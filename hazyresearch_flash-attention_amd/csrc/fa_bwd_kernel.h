@@ -74,15 +74,16 @@ struct BwdCfg {
 // apart per half-wave) touch every bank once.
 __device__ __forceinline__ int ds_off(int r, int q) { return r * 64 + ((q * 2) ^ (((r >> 1) & 7) << 3)); }
 
-// delta = rowsum(dO * O) (softmax_d), and zero the fp32 dQ accumulator (if any). 16 threads per row
-// (one 16-B chunk each), 16 rows per 256-thread block, shuffle reduction over the 16 lanes.
-template <typename T>
+// delta = rowsum(dO * O) (softmax_d), and zero the fp32 dQ accumulator (if any). CPR threads per
+// row (one 16-B chunk each; CPR = head_dim / 8 rounded up to 4, 8 or 16, so no lane idles at D = 32
+// or 64), 256 / CPR rows per 256-thread block, shuffle reduction over the CPR lanes.
+template <typename T, int CPR>
 __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const FaBwdArgs a) {
     const int b = blockIdx.z, h = blockIdx.y;
     const int q_start = a.cu_seqlens_q[b];
     const int seqlen_q = a.cu_seqlens_q[b + 1] - q_start;
-    const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
-    const int c = threadIdx.x & 15;
+    const int row = blockIdx.x * (256 / CPR) + (threadIdx.x / CPR);
+    const int c = threadIdx.x % CPR;
     const bool ok = row < seqlen_q && c * 8 < a.head_dim;
     float sum = 0.f;
     if (ok) {
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const FaBwdArgs a) {
         }
     }
 #pragma unroll
-    for (int w = 8; w >= 1; w >>= 1) sum += __shfl_xor(sum, w, 16);
+    for (int w = CPR / 2; w >= 1; w >>= 1) sum += __shfl_xor(sum, w, CPR);
     if (c == 0 && row < seqlen_q) a.softmax_d[(int64_t)(b * a.nheads + h) * a.lse_stride + row] = sum;
 }
 
