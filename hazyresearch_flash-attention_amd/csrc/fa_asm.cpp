@@ -222,7 +222,10 @@ hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
     k.nbh = (uint32_t)a.nheads * (uint32_t)a.batch;
     k.causal = a.is_causal ? 1u : 0u;
     k.magic_nbh = magic_half(k.nbh);
-    if (a.is_causal && k.nbh % 8 == 0) {
+    // causal XCD groups only for the D=128 tile (its 2 MB of K/V per head at S=4096 want one L2): at
+    // D=64 the global heaviest-first order measured faster (tools/asm_group_ab.py, B8 H12 S2048: 69.3
+    // vs 75.4-90.3 us for G = 1..4; C4 D=128: G = 4 764.8 vs 836.4 us global)
+    if (a.is_causal && k.nbh % 8 == 0 && a.head_dim > 64) {
         // G nqb ~ 2x the workgroups one XCD runs at once (one per CU: 32), G dividing the XCD's
         // nbh / 8 heads so that every group is full (the HIP kernels' measured choice, x2 slots)
         const uint32_t nh = k.nbh / 8, want = (64 + nqb - 1) / nqb;
