@@ -150,7 +150,7 @@ def configure(hd, waves=4):
     global V_KADDR, V_VADDR, V_DMA, V_S, V_P, V_MTHR, V_MC, V_TMP, V_BPA, V_BPL, V_NEGINF, V_NVREL, V_ROW1
     global V_OOFF, V_LOFF, V_ONEF, V_LANE, V_ETMP, V_MCB, NVGPR, A_O, A_L, A_ONES, A_Q, A_KF, A_VF, NAGPR
     global NWAVES, BLOCKS, NETMP, V_ORT, V_EPT, EXP_LAG, CVT_LAG
-    assert hd in (64, 128) and waves in (4, 8)
+    assert hd in (32, 64, 128) and waves in (4, 8)
     globals().update(_D64)   # the D = 64 layout, then the D = 128 / 8-wave changes
     globals().update(PERSIST=False, KARG_BYTES=168)
     EXP_LAG, CVT_LAG = 4, 4
@@ -180,6 +180,14 @@ def configure(hd, waves=4):
         return
     NWAVES, BLOCKS, NETMP, V_ORT, V_EPT = 4, 'AB', 16, None, None
     if hd == 64:
+        return
+    if hd == 32:
+        # D = 32 (head_dim <= 32, zero-padded): the D = 64 register map with half-size K / V^T fragment
+        # buffers, one O d-block, one 1-KiB DMA piece per tensor, tile and wave (4 KiB tiles)
+        D, NKS, NDT, NP, ROWB, KFB = 32, 2, 1, 1, 64, 16
+        TILE = BN * D * 2
+        VREG = R * TILE
+        LDS_BYTES = 2 * R * TILE
         return
     D, NKS, NDT, NP, ROWB, KFB = hd, hd // 16, hd // 32, hd // 32, 2 * hd, hd // 2
     NBK = NBV = 1
@@ -215,7 +223,7 @@ def epi_regs(X, idx):
     words in registers dead by then. D = 64: S_X and P_X. D = 128 (8 slots): S_A..S_B for the fp32
     (both softmaxes are done); the words of block A in P_A then the exp temporaries (P_B still
     feeds the last P_B.V beside it), of block B in P_A..P_B."""
-    if D == 64:
+    if D <= 64:
         return V_S[X] + 8 * idx, V_P[X] + 4 * idx
     E = V_S['A'] + 8 * idx
     if X == 'A' and idx >= 4:
@@ -348,6 +356,8 @@ class Gen:
                 if si < 4 and 'nosum' not in PROBE:
                     out.append(sums[si])
                     si += 1
+        if 'nosum' not in PROBE:
+            out += sums[si:]     # D = 32: one d-block leaves two row-sum MFMAs
         return out, use
 
     # ------------------------------------------------------------------ LDS reads / DMA
@@ -1122,6 +1132,8 @@ def S(txt, rd=(), wr=(), kind='salu'):
 def xfun(dst, r, t1, t2):
     """x(r) of the LDS swizzle (fa_common.h Swz<D>): D = 64: u = (r>>1)&7, x = ((u&1)<<2)|(u>>1);
     D = 128: x = ((r&3)<<2)|((r>>2)&3)."""
+    if D == 32:
+        return [V(f'v_bfe_u32 v{dst}, v{r}, 2, 2', dst, [r])]
     lo = (1, 1) if D == 64 else (0, 2)
     return [V(f'v_bfe_u32 v{t1}, v{r}, {lo[0]}, {lo[1]}', t1, [r]),
             V(f'v_lshlrev_b32 v{t1}, 2, v{t1}', t1, [t1]),
@@ -1441,7 +1453,7 @@ def set_persist(on):
         assert NWAVES == 4 and not MC_BANKS
         # D = 128: Q, row sums and the indicator fill the VGPRs (no room for the next Q): K/V tail
         # only, the workitem id in the last free VGPR
-        PERSIST_Q = D == 64
+        PERSIST_Q = D <= 64
         V_TID = 208 if PERSIST_Q else 251
         NVGPR = max(NVGPR, NVGPR_PERSIST if PERSIST_Q else V_TID + 1)
         N_STORES = len(BLOCKS) * (1 + 2 * NDT)
@@ -1831,7 +1843,7 @@ def expand_regs(spec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f16'])
-    ap.add_argument('--hd', type=int, default=64, choices=[64, 128], help='head-dim tile')
+    ap.add_argument('--hd', type=int, default=64, choices=[32, 64, 128], help='head-dim tile')
     ap.add_argument('--waves', type=int, default=4, choices=[4, 8], help='waves per workgroup (8: D = 64 only)')
     ap.add_argument('--prio4', type=int, default=None, help='8 waves: s_setprio 1 for waves 4-7')
     ap.add_argument('--persist', type=int, default=0, help='persistent workgroups: next-block K/V tail (and next-Q prefetch at D = 64), 4 waves')

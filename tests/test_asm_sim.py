@@ -70,7 +70,7 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4,
     if grid:
         karg += struct.pack("<2I", grid, 0)
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
-    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64, waves, bool(grid)), dtype).run(
+    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64 if D > 32 else 32, waves, bool(grid)), dtype).run(
         (grid, 1, 1) if grid else (nqb, H, B), pa, mem)
     o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
     lse = mem.get(pl).view(np.float32).reshape(B, H, lse_stride)
@@ -152,7 +152,7 @@ def test_asm_forward_rescale_path_in_simulator():
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 @pytest.mark.parametrize("hd,waves,persist", [(64, 4, False), (128, 4, False), (64, 8, False), (64, 4, True),
-                                               (128, 4, True)])
+                                               (128, 4, True), (32, 4, False), (32, 4, True)])
 def test_generated_kernel_assembles(dtype, hd, waves, persist, tmp_path):
     """The simulator does not check encodings (register alignment, gfx950 operand forms): the
     product kernels must also assemble for gfx950, as build.py does."""
@@ -206,3 +206,19 @@ def test_asm_forward_persistent_in_simulator(lens_q, lens_k, H, D, grid, dtype):
 def test_asm_forward_persistent_d128_in_simulator(lens_q, lens_k, H, grid):
     """The persistent form at head_dim = 128 (K/V tail only: Q stays in VGPRs, no next-Q prefetch)."""
     _run(lens_q, lens_k, H, 128, "bf16", grid=grid)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("lens_q,lens_k,H,D", [
+    ([130], [200], 1, 32),            # 3 full tiles + a masked one
+    ([70, 33], [700, 0], 1, 32),      # 11 tiles (every loop position, last-tile exit); empty key set
+    ([257, 40], [33, 190], 2, 16),    # head_dim 16 zero-padded into the D = 32 tile; var-len
+])
+def test_asm_forward_d32_in_simulator(lens_q, lens_k, H, D, dtype):
+    """The head_dim <= 32 tile (one O d-block, 4-KiB K / V tiles, two 16-deep k-steps)."""
+    _run(lens_q, lens_k, H, D, dtype)
+
+
+def test_asm_forward_d32_causal_and_persistent_in_simulator():
+    _run([300], [300], 1, 32, "bf16", causal=True)
+    _run([300, 200], [512, 256], 2, 24, "bf16", grid=2)

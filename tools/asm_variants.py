@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--shape", default="8,12,2048")
     ap.add_argument("--variants", default=",nomax,noexp,nofma,nocvt,nofill,nodma,nolds,nosum,nobar")
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--hd", type=int, default=64, choices=[64, 128])
+    ap.add_argument("--hd", type=int, default=64, choices=[32, 64, 128])
     ap.add_argument("--iters", type=int, default=50)
     args = ap.parse_args()
     out = os.path.join(ROOT, "gpurun_out")
