@@ -1386,7 +1386,7 @@ def prologue_sections(g):
     p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
     # (8 waves: phase 0 reads K2 as well: K0 K1 V0 K2 landed, all but the 3 youngest pieces)
-    p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else 4 * (DIST - 1)})'), raw('s_barrier')]
+    p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else pieces_wait()})'), raw('s_barrier')]
     p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
     # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
     p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
@@ -1520,7 +1520,7 @@ def prologue_persist(g):
         return st
     # the first wait waits for Q, K0, K1, V0: younger are K2 V1 K3 V2 (8 pieces) and the next Q's loads
     pb2 = [label('.Lqdone'), S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + sc['dma'] + pf + \
-        sc['zero'] + start_with_wait(4 * (DIST - 1) + nq)
+        sc['zero'] + start_with_wait(pieces_wait() + nq)
     # K0..K3 / V0..V2 came from the previous block's tail: the descriptor sets only walk as the
     # prologue's DMAs would have; younger than K0 K1 V0 are the tail's last 8 pieces, this
     # block's 2 x 5 O / LSE stores per wave and the next Q's loads
@@ -1638,7 +1638,14 @@ def tile_vmcnt():
     """vmcnt of the wait before each tile's barrier: the 4-wave form needs K(t+2), V(t+1) in LDS
     for the next tile (all but the DMAs of the last DIST - 1 tiles); the 8-wave form reads K(t+2)
     one tile earlier (all but this tile's two pieces)."""
-    return 2 * NP * (DIST - 2) if NWAVES == 8 else 4 * (DIST - 1)
+    return 2 * NP * (DIST - 2) if NWAVES == 8 else pieces_wait()
+
+
+def pieces_wait():
+    """4-wave form: DMA pieces that may stay in flight when the next tile starts: the last DIST - 1
+    tiles' (2 NP each; D = 32 has NP = 1 and needs exactly this). At D = 128 (NP = 4) the stricter
+    4 (DIST - 1) stays: measured even against 2 NP (DIST - 1) (tools/wait_ab.sh)."""
+    return min(2 * NP, 4) * (DIST - 1)
 
 
 def tile_phases(g, t, **kw):
