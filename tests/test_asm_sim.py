@@ -150,9 +150,9 @@ def test_asm_forward_rescale_path_in_simulator():
     _run([70], [300], 1, 64, "bf16", scale=3.0)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("hd,waves,persist", [(64, 4, False), (128, 4, False), (64, 8, False), (64, 4, True),
-                                               (128, 4, True), (32, 4, False), (32, 4, True)])
+@pytest.mark.parametrize("dtype,hd,waves,persist", [
+    (dt, hd, w, p) for dt in ("bf16", "f16") for hd, w, p in ((64, 4, False), (128, 4, False), (64, 8, False))] + [
+    ("bf16", 64, 4, True), ("bf16", 128, 4, True), ("bf16", 32, 4, False)])   # (f16 persistent: build.py assembles it)
 def test_generated_kernel_assembles(dtype, hd, waves, persist, tmp_path):
     """The simulator does not check encodings (register alignment, gfx950 operand forms): the
     product kernels must also assemble for gfx950, as build.py does."""
