@@ -1720,7 +1720,11 @@ def build(g):
     masks = [masked_tile(g, t, rescue) for t in range(U)]
     lasts = [last_tile(g, t, rescue) for t in range(U)]
     empty = [label('.Lempty')] + sum(([mark()] + g.epilogue(X) for X in BLOCKS), []) + \
-            ([raw('s_branch .Lseam')] if PERSIST else [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')])
+            ([raw('s_waitcnt vmcnt(0)'), raw('s_branch .Lseam')] if PERSIST else [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')])
+    # (PERSIST: an empty key set may follow a tail that prefetched its (zero-length) K/V: drain before
+    # the next block's DMAs reuse the ring. The loop's own past-the-end DMAs of a block without a tail
+    # read nothing (num_records 0: zero-filled, no memory access) and were issued a tile or more
+    # before the seam; every GPU form test mixes both kinds of seams.)
     end = [label('.Lend'), raw('s_endpgm')]
     if PERSIST:
         # .Lend (q-block past its sequence: nothing prefetched) and .Lseam (after a block): next block
