@@ -167,13 +167,13 @@ def test_generated_kernel_assembles(dtype, hd, waves, persist, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("lens_q,lens_k,causal", [
-    ([130], [200], False),            # 3 full tiles + a masked one, rows past the block end
-    ([257, 40], [33, 190], False),    # var-len, two q-blocks, single masked tile
-    ([70], [700], False),             # 11 tiles: every unrolled loop position and its last-tile exit
-    ([40, 64], [0, 65], False),       # empty key set (zeros, -inf)
-    ([300], [300], True),             # causal: the diagonal band of two q-blocks
+@pytest.mark.parametrize("lens_q,lens_k,causal,dtype", [
+    ([130], [200], False, "bf16"),            # 3 full tiles + a masked one, rows past the block end
+    ([257, 40], [33, 190], False, "bf16"),    # var-len, two q-blocks, single masked tile
+    ([70], [700], False, "bf16"),             # 11 tiles: every unrolled loop position and its last-tile exit
+    ([70], [700], False, "f16"),              # (fp16: the rescale delta of 2, frequent rescales)
+    ([40, 64], [0, 65], False, "bf16"),       # empty key set (zeros, -inf)
+    ([300], [300], True, "bf16"),             # causal: the diagonal band of two q-blocks
 ])
 def test_asm_forward_w8_in_simulator(lens_q, lens_k, causal, dtype):
     """The two-waves-per-SIMD form (8 waves, one 32-row block per wave, head_dim == 64)."""
@@ -185,13 +185,13 @@ def test_asm_forward_w8_rescale_path_in_simulator():
     _run([70], [300], 1, 64, "bf16", scale=3.0, waves=8)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("lens_q,lens_k,H,D,grid", [
-    ([130], [200], 3, 64, 1),             # one workgroup walks all 3 blocks (next-Q prefetch each time)
-    ([257, 40], [33, 190], 2, 64, 3),     # var-len, 3 workgroups over 8 blocks: empty q-blocks (.Lend)
-    ([70, 300], [700, 0], 2, 48, 2),      # 11 tiles, empty key set, head_dim < 64 (masked Q chunks)
-    ([300, 200], [512, 256], 2, 64, 1),   # nt = 8 and 4: the tail streams the next block's K/V tiles
-    ([300, 100], [512, 320], 2, 64, 3),   # tails into a next block with nt % 4 != 0, and into an empty q-block
+@pytest.mark.parametrize("lens_q,lens_k,H,D,grid,dtype", [
+    ([130], [200], 3, 64, 1, "bf16"),             # one workgroup walks all 3 blocks (next-Q prefetch each time)
+    ([257, 40], [33, 190], 2, 64, 3, "bf16"),     # var-len, 3 workgroups over 8 blocks: empty q-blocks (.Lend)
+    ([70, 300], [700, 0], 2, 48, 2, "bf16"),      # 11 tiles, empty key set, head_dim < 64 (masked Q chunks)
+    ([300, 200], [512, 256], 2, 64, 1, "bf16"),   # nt = 8 and 4: the tail streams the next block's K/V tiles
+    ([300, 200], [512, 256], 2, 64, 1, "f16"),
+    ([300, 100], [512, 320], 2, 64, 3, "bf16"),   # tails into a next block with nt % 4 != 0, and into an empty q-block
 ])
 def test_asm_forward_persistent_in_simulator(lens_q, lens_k, H, D, grid, dtype):
     """The persistent form (one workgroup walks blocks L, L + grid, ...; the next block's Q is
