@@ -148,10 +148,14 @@ int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
         return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: impl must be one of FA_IMPL_AUTO / HIP / ASM4 / ASM8 / ASM4P");
     if (a->max_seqlen_q == 0) return FA_OK;
     hipStream_t s = (hipStream_t)stream;
-    hipError_t e;
-    if (fa::fwd_asm_eligible(*a, bm)) {
-        e = fa::launch_fwd_asm(*a, s);
-    } else switch (pick_tile(a->head_dim)) {
+    hipError_t e = hipSuccess;
+    bool asm_unavailable = false;
+    if (fa::fwd_asm_eligible(*a, bm)) e = fa::launch_fwd_asm(*a, s, &asm_unavailable);
+    // FA_IMPL_AUTO falls back to the HIP kernels when the code objects cannot be loaded (first call
+    // of a device inside a capture that refuses module loads); a forced asm form reports it
+    if (asm_unavailable && a->impl != FA_IMPL_AUTO)
+        return fail(FA_ERR_UNSUPPORTED, "fa_fwd: the assembly kernels could not be loaded on this device");
+    if (!fa::fwd_asm_eligible(*a, bm) || asm_unavailable) switch (pick_tile(a->head_dim)) {
         case 32: e = fa::launch_fwd<32>(*a, bm, s); break;
         case 64: e = fa::launch_fwd<64>(*a, bm, s); break;
         default: e = fa::launch_fwd<128>(*a, bm, s); break;

@@ -92,6 +92,36 @@ struct DevFns {
 std::mutex g_mu;
 DevFns g_fns[kMaxDev];
 
+// Every form of the device is loaded at its first asm call, under the mutex, so that after any one
+// eager call no later call (whatever form its grid picks) loads a module: a call inside a hipGraph
+// capture then only launches. If the very first asm call of a device happens inside a capture, the
+// loads run with this thread's capture mode exchanged to relaxed (module loading is not a stream
+// operation; in global mode the runtime may refuse it), and if they still fail the caller falls back
+// to the HIP kernels (fa_api.cpp) instead of failing the capture.
+hipError_t load_all(DevFns &d) {
+    static const void *const imgs[kNumFns] = {fa_asm_fwd_d64_bf16,   fa_asm_fwd_d64_f16,
+                                              fa_asm_fwd_d128_bf16,  fa_asm_fwd_d128_f16,
+                                              fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16,
+                                              fa_asm_fwd_d64p_bf16,  fa_asm_fwd_d64p_f16,
+                                              fa_asm_fwd_d128p_bf16, fa_asm_fwd_d128p_f16};
+    static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
+                                               "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
+                                               "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
+                                               "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
+                                               "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm"};
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    const bool exchanged = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < kNumFns && e == hipSuccess; ++k) {
+        if (d.fn[k]) continue;
+        e = hipModuleLoadData(&d.mod[k], imgs[k]);
+        if (e == hipSuccess) e = hipModuleGetFunction(&d.fn[k], d.mod[k], names[k]);
+        if (e != hipSuccess) d.fn[k] = nullptr;
+    }
+    if (exchanged) hipThreadExchangeStreamCaptureMode(&mode);
+    return e;
+}
+
 hipError_t get_function(int dtype, int form, hipFunction_t *out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -101,22 +131,8 @@ hipError_t get_function(int dtype, int form, hipFunction_t *out) {
     std::lock_guard<std::mutex> lk(g_mu);
     DevFns &d = g_fns[dev];
     if (!d.fn[k]) {
-        static const void *const imgs[kNumFns] = {fa_asm_fwd_d64_bf16,   fa_asm_fwd_d64_f16,
-                                                  fa_asm_fwd_d128_bf16,  fa_asm_fwd_d128_f16,
-                                                  fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16,
-                                                  fa_asm_fwd_d64p_bf16,  fa_asm_fwd_d64p_f16,
-                                                  fa_asm_fwd_d128p_bf16, fa_asm_fwd_d128p_f16};
-        static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
-                                                   "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
-                                                   "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
-                                                   "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
-                                                   "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm"};
-        const void *img = imgs[k];
-        const char *name = names[k];
-        e = hipModuleLoadData(&d.mod[k], img);
-        if (e != hipSuccess) return e;
-        e = hipModuleGetFunction(&d.fn[k], d.mod[k], name);
-        if (e != hipSuccess) return e;
+        e = load_all(d);
+        if (e != hipSuccess || !d.fn[k]) return e != hipSuccess ? e : hipErrorNotFound;
     }
     *out = d.fn[k];
     return hipSuccess;
@@ -184,14 +200,19 @@ static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
     return nwg > (uint32_t)g ? g : 0;
 }
 
-hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream) {
+hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavailable) {
     hipFunction_t fn = nullptr;
+    *unavailable = false;
     const bool w8 = use_w8(a);
     const uint32_t nqb0 = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
     const int pgrid = w8 ? 0 : persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
     const bool d128 = a.head_dim > 64;
     hipError_t e = get_function(a.dtype, w8 ? 2 : pgrid ? (d128 ? 4 : 3) : (d128 ? 1 : 0), &fn);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) {
+        (void)hipGetLastError();   // the load error is not the caller's launch error
+        *unavailable = true;
+        return hipSuccess;
+    }
     FaAsmFwdArgs k;
     std::memset(&k, 0, sizeof(k));
     k.q = a.q;

@@ -38,7 +38,9 @@ hipError_t launch_zero_seq_rows(void *base, const int32_t *cu, int64_t row_strid
                                 int nheads, int head_dim, int max_seqlen, hipStream_t s);
 // hand-scheduled assembly forward (fa_asm.cpp, csrc/asm/gen_fwd.py)
 bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm);
-hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream);
+// *unavailable is set (and hipSuccess returned, nothing launched) when the device's code objects
+// could not be loaded: the caller then runs the HIP kernels (fa_asm.cpp load_all).
+hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavailable);
 
 // Raise a kernel's dynamic-LDS limit once per (kernel, device): the attribute is per device, so
 // a process that launches on several GPUs sets it on each. `done` is the call site's own bit set

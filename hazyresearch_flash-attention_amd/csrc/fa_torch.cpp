@@ -186,7 +186,13 @@ at::Tensor bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Te
     TORCH_CHECK(rows_ok(dk), "dk must have contiguous last dimension and non-overlapping rows");
     TORCH_CHECK(rows_ok(dv), "dv must have contiguous last dimension and non-overlapping rows");
     TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous(), "softmax_lse must be fp32 contiguous");
+    TORCH_CHECK(lse.is_cuda() && q.is_cuda(), "softmax_lse and q must be on the GPU");
+    TORCH_CHECK(cu_q.scalar_type() == at::kInt && cu_k.scalar_type() == at::kInt, "cu_seqlens must be int32");
+    TORCH_CHECK(cu_q.is_cuda() && cu_k.is_cuda(), "cu_seqlens must be on the GPU");
+    TORCH_CHECK(cu_q.is_contiguous() && cu_k.is_contiguous(), "cu_seqlens must be contiguous");
+    TORCH_CHECK(cu_k.numel() == cu_q.numel(), "cu_seqlens_k must have shape (batch_size + 1)");
     const int64_t batch = cu_q.numel() - 1;
+    TORCH_CHECK(batch > 0, "batch_size must be positive");
     const int64_t total_q = q.size(0), nheads = q.size(1), head_dim = q.size(2);
     TORCH_CHECK(head_dim % 8 == 0 && head_dim <= 128, "head_size must be a multiple of 8 and <= 128");
     TORCH_CHECK(dq.sizes() == q.sizes() && dout.sizes() == q.sizes() && out.sizes() == q.sizes(),

@@ -121,18 +121,25 @@ class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
 
 
 _cu_cache = {}
+_CU_CACHE_MAX = 256
 
 
 def _uniform_cu_seqlens(B, S, device):
     """cu_seqlens of B sequences of length S (cached per shape and device: one arange launch per
-    shape instead of one per call; the tensor is only read by the kernels)."""
+    shape instead of one per call; the tensor is only read by the kernels).
+
+    Graph safety: entries are never evicted (a captured graph may hold the address of a cached
+    tensor; freeing it would let replays read reused memory as sequence bounds), past the cap new
+    shapes simply get a fresh tensor; and while the current stream is capturing, the tensor is made
+    fresh inside the capture (its arange is replayed with the graph) and not cached, so an eager
+    call never sees graph-pool memory that only a replay initialises."""
+    capturing = device.type == "cuda" and torch.cuda.is_current_stream_capturing()
     key = (B, S, device)
-    cu = _cu_cache.get(key)
+    cu = None if capturing else _cu_cache.get(key)
     if cu is None:
         cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=device)
-        if len(_cu_cache) > 64:
-            _cu_cache.clear()
-        _cu_cache[key] = cu
+        if not capturing and len(_cu_cache) < _CU_CACHE_MAX:
+            _cu_cache[key] = cu
     return cu
 
 

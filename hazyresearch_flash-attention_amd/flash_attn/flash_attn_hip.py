@@ -501,6 +501,11 @@ def bwd(dout, q, k, v, out, softmax_lse, dq, dk, dv, cu_seqlens_q, cu_seqlens_k,
     for t, n in ((dq, "dq"), (dk, "dk"), (dv, "dv")):
         _check(_rows_ok(t), f"{n} must have contiguous last dimension and non-overlapping rows")
     _check(softmax_lse.dtype == torch.float32 and softmax_lse.is_contiguous(), "softmax_lse must be fp32 contiguous")
+    _check(softmax_lse.is_cuda and q.is_cuda, "softmax_lse and q must be on the GPU")
+    _check(cu_seqlens_q.dtype == torch.int32 and cu_seqlens_k.dtype == torch.int32, "cu_seqlens must be int32")
+    _check(cu_seqlens_q.is_cuda and cu_seqlens_k.is_cuda, "cu_seqlens must be on the GPU")
+    _check(cu_seqlens_q.is_contiguous() and cu_seqlens_k.is_contiguous(), "cu_seqlens must be contiguous")
+    _check(cu_seqlens_k.numel() == cu_seqlens_q.numel(), "cu_seqlens_k must have shape (batch_size + 1)")
     batch = cu_seqlens_q.numel() - 1
     total_q, nheads, head_dim = q.shape
     _check(head_dim % 8 == 0 and head_dim <= 128, "head_size must be a multiple of 8 and <= 128")

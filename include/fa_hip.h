@@ -20,8 +20,11 @@
  *   fa_index_add_first_axis <- IndexFirstAxisResidual.backward (flash_attn/bert_padding.py:82-94)
  *   fa_rotary               <- apply_rotary_pos_emb + RotaryEmbedding(2D).forward and their autograd
  *                              backward (flash_attn/rotary.py:22-41, 86-135)
- *   (fa_fwd's D=64 non-causal shapes run a hand-scheduled gfx950 assembly kernel, csrc/asm/gen_fwd.py,
- *    embedded in the library as a code object; FaFwdArgs.impl selects it or the HIP kernels)
+ *   (fa_fwd runs hand-scheduled gfx950 assembly kernels, csrc/asm/gen_fwd.py, embedded in the library
+ *    as code objects, for head_dim in (32, 64] or == 128, fp16/bf16, causal or not, no dropout, dense,
+ *    no fused rotary; the persistent form for
+ *    non-causal grids with more blocks than CUs (fa_asm.cpp fwd_asm_eligible / persistent_grid_for).
+ *    FaFwdArgs.impl selects a form or the HIP kernels.)
  *   fa_query, fa_last_error, fa_version: host helpers (no reference counterpart; the reference
  *                                                  raised through TORCH_CHECK / exit(1),
  *                                                  fmha_api.cpp:131-170, fmha_utils.h:36-48)
@@ -30,12 +33,16 @@
  *   - Plain C types only: raw device pointers, element strides (int64), sizes. No torch types.
  *   - The caller allocates every output and workspace (the Python layer uses torch.empty).
  *   - Every call is stream-ordered and asynchronous on `stream` (a hipStream_t, NULL = default).
- *     No host synchronisation, no allocation, no exit(), so calls can be captured into a
- *     hipGraph. Dropout under capture: a captured (seed, rng_offset) is a constant, so pass
+ *     No host synchronisation, no device allocation, no exit(), so calls can be captured into a
+ *     hipGraph. One-time state: the first assembly-kernel call on a device loads all of that
+ *     device's code objects (hipModuleLoadData, under a mutex, capture mode exchanged to relaxed);
+ *     if that first call is inside a capture and the load fails, FA_IMPL_AUTO runs the HIP kernels
+ *     instead. One eager call before capturing avoids both. Dropout under capture: a captured (seed, rng_offset) is a constant, so pass
  *     rng_offset_dev pointing at a device word that the graph advances before each launch
  *     (flash_attn_hip.py does this), or every replay draws the same mask.
  *   - Return 0 on success; non-zero = error, with a message in fa_last_error() (thread-local).
- *   - No global mutable state: concurrent calls from several host threads are safe.
+ *   - The only global mutable state is that per-device code-object table (mutex-guarded) and the
+ *     cached CU count: concurrent calls from several host threads are safe.
  *
  * Layout ("unpadded", reference fmha_api.cpp:113-115,149-151): q is (total_q, H, D), k/v are
  * (total_k, H, D), with stride(-1) == 1 and arbitrary row/head strides (packed qkv/kv views).

@@ -86,3 +86,39 @@ def test_asm_form_forward_d128(form, seqlen_q, seqlen_k):
     hip = _hip()
     with hip.force_impl(getattr(hip, f"FA_IMPL_{form}")):
         run_case("separate", 6, seqlen_q, seqlen_k, 8, 128, torch.bfloat16, False, 0.0, grad=False, seed=seqlen_k)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_asm_persistent_empty_key_set_after_tail(d):
+    """the persistent form's .Lempty path right after a block that took the K/V tail
+    (key counts that are multiples of 4 tiles alternate with empty key sets), with more blocks than
+    CUs: empty rows give out == 0 and lse == -inf, every other row matches the oracle."""
+    import numpy as np
+    from flash_attn import flash_attn_interface as fi
+    from oracle.attention_ref import ulp_floor
+    hip = _hip()
+    B, H = 48, 8
+    lens_q = [300] * B
+    lens_k = [1024 if b % 2 == 0 else 0 for b in range(B)]
+    cu_q = torch.tensor([0] + list(np.cumsum(lens_q)), dtype=torch.int32, device=DEV)
+    cu_k = torch.tensor([0] + list(np.cumsum(lens_k)), dtype=torch.int32, device=DEV)
+    g = torch.Generator().manual_seed(d)
+    q = torch.randn(sum(lens_q), H, d, generator=g).bfloat16().to(DEV)
+    k = torch.randn(sum(lens_k), H, d, generator=g).bfloat16().to(DEV)
+    v = torch.randn(sum(lens_k), H, d, generator=g).bfloat16().to(DEV)
+    with hip.force_impl(hip.FA_IMPL_ASM4P):
+        out, lse, _ = fi.flash_attn_unpadded_func(q, k, v, cu_q, cu_k, max(lens_q), max(lens_k), 0.0,
+                                                  return_attn_probs=True)
+    torch.cuda.synchronize()
+    for b in range(B):
+        qs, ks = slice(int(cu_q[b]), int(cu_q[b + 1])), slice(int(cu_k[b]), int(cu_k[b + 1]))
+        if lens_k[b] == 0:
+            assert (out[qs] == 0).all(), b
+            assert torch.isinf(lse[b, :, :lens_q[b]]).all() and (lse[b, :, :lens_q[b]] < 0).all(), b
+            continue
+        if b % 8:     # the oracle on a sample of the non-empty sequences
+            continue
+        ref, _ = attention_ref(q[qs][None], k[ks][None], v[ks][None])
+        pt, _ = attention_ref(q[qs][None], k[ks][None], v[ks][None], upcast=False, reorder_ops=True)
+        err = (out[qs].float() - ref[0].float()).abs().max().item()
+        assert err <= max_err_bound(pt, ref, floor=ulp_floor(ref)), (b, err)

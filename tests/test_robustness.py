@@ -136,3 +136,74 @@ def test_dropout_under_graph_capture_advances_the_stream():
         assert torch.equal(out, eager)
         outs.append(out.clone())
     assert not torch.equal(outs[0], outs[1])
+
+
+def test_rotary_graph_replay_after_cu_seqlens_cache_churn():
+    """a graph captured around the fused-rotary forward keeps reading valid sequence
+    bounds after the host cu_seqlens cache has seen hundreds of other shapes (the capture makes
+    its own cu_seqlens inside the graph; cached entries are never freed)."""
+    from flash_attn import flash_attention as fam
+    from oracle.rotary_ref import rotary_tables
+    B, S, H, D = 2, 200, 2, 64
+    g = torch.Generator().manual_seed(4)
+    qkv = torch.randn(B, S, 3, H, D, generator=g).bfloat16().to(DEV)
+    cos, sin = (t.to(DEV) for t in rotary_tables(S, D, torch.bfloat16))
+    eager = fam.FlashAttnRotaryQKVFunc.apply(qkv, cos, sin, 0.0, None, False).clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fam.FlashAttnRotaryQKVFunc.apply(qkv, cos, sin, 0.0, None, False)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = fam.FlashAttnRotaryQKVFunc.apply(qkv, cos, sin, 0.0, None, False)
+    for n in range(1, 301):     # churn: more shapes than the cache holds
+        fam._uniform_cu_seqlens(n % 7 + 1, n, qkv.device)
+    junk = [torch.full((4096,), -1, dtype=torch.int32, device=DEV) for _ in range(64)]
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
+    del junk
+    # a call after the capture, same shape, eager: its cached bounds are initialised
+    again = fam.FlashAttnRotaryQKVFunc.apply(qkv, cos, sin, 0.0, None, False)
+    assert torch.equal(again, eager)
+
+
+_FRESH_CAPTURE = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+from flash_attn import flash_attn_interface as fi
+from oracle.attention_ref import attention_ref, max_err_bound
+B, S, H, d = 2, 600, 4, 64
+g = torch.Generator().manual_seed(9)
+q, k, v = (torch.randn(B * S, H, d, generator=g).bfloat16().cuda() for _ in range(3))
+cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device="cuda")
+torch.cuda.synchronize()
+graph = torch.cuda.CUDAGraph()
+with torch.cuda.graph(graph):       # the process's first attention call
+    out = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
+graph.replay()
+torch.cuda.synchronize()
+qb, kb, vb = (t.view(B, S, H, d) for t in (q, k, v))
+ref, _ = attention_ref(qb, kb, vb)
+pt, _ = attention_ref(qb, kb, vb, upcast=False, reorder_ops=True)
+err = (out.view(B, S, H, d).float() - ref.float()).abs().max().item()
+assert err <= max_err_bound(pt, ref), err
+eager = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
+torch.cuda.synchronize()
+print("ok", err, bool(torch.equal(eager, out)))
+"""
+
+
+def test_first_forward_of_a_process_inside_graph_capture():
+    """a fresh process whose first forward is captured (the asm code objects are
+    loaded inside the capture, or the call falls back to the HIP kernels) replays correctly."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "hazyresearch_flash-attention_amd")
+    r = subprocess.run([sys.executable, "-c", _FRESH_CAPTURE, pkg, root], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.strip().splitlines()[-1].startswith("ok")
