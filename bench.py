@@ -156,12 +156,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        # replicas only: the barrier and the max-of-elapsed reduction are host-side (gloo, CPU
+        # tensors); no RCCL communicator is created (north_star: no collective on the data path)
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        dist.init_process_group(backend="gloo")
     dev = torch.device(f"cuda:{local_rank}")
     torch.cuda.set_device(dev)
 
+    from flash_attn import flash_attn_hip
     from flash_attn.flash_attn_interface import flash_attn_unpadded_func, flash_attn_unpadded_kvpacked_func
 
     B, H, S, D = 8, 12, 2048, 64
@@ -195,7 +198,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
     value = world * flops * args.steps / el / 1e12
@@ -207,7 +210,7 @@ def main():
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": read_traffic(),
                 "measured_mfma_ceiling": MFMA_CEILING_RANDOM_TFLOPS,
                 "frac_of_measured_ceiling": round(achieved / MFMA_CEILING_RANDOM_TFLOPS, 4),
-                "kernel": "fa_fwd_d64p_bf16_asm (csrc/asm/gen_fwd.py --persist 1)", "avg_kernel_ms": round(avg_ms, 4),
+                "kernel": flash_attn_hip.fwd_kernel_name(B, H, D, S, S, dtype), "avg_kernel_ms": round(avg_ms, 4),
                 "flops_per_launch": flops, "algorithmic_bytes_per_launch": fwd_bytes(B, H, S, S, D)}
 
     extra = {}

@@ -64,6 +64,13 @@ ORDET_DELTA = {'bf16': 8.0, 'f16': 2.0}   # a rescale sets m = tile max * c + de
 EXP_LAG = 4            # exp_stream: fma(i) -> exp(i) distance (instructions)
 CVT_LAG = 4            # exp_stream: exp -> cvt distance
 MC_BANKS = False       # fma reads m*c from one of 4 copies in a VGPR bank other than its S operand
+PRESCALE = False       # Q pre-multiplied by c (rounded to the 16-bit type once per block) and S^T seeded
+#                        with -m c (16 registers per block): the softmax is exp2(S), no per-element fma
+SEED0 = 4096.0         # initial -m c: every tile 0 fires the rescale unless all its scores are < -3968
+V_SEED = {'A': 212, 'B': 228}   # PRESCALE: -m c broadcast over the 16 registers of an S^T tile
+KFIRST = False         # phase 1: K(t+1) fragment reads ahead of the V^T reads (D = 64)
+KFIRST_LO = 2          # softmax-stream position of the first K read with KFIRST
+LGKM_XPHASE = False    # counted lgkmcnt waits may count LDS reads of the previous phase
 
 
 def set_geometry(r, dist):
@@ -325,10 +332,11 @@ class Gen:
             acc = S + 16 * st
             for ks in range(NKS):
                 kf = A_KF + KFB * (t % NBK) + 4 * (st * NKS + ks)
-                c = '0' if ks == 0 else vs(acc, 16)
+                seed = PRESCALE and ks == 0
+                c = (vs(V_SEED[X], 16) if seed else '0') if ks == 0 else vs(acc, 16)
                 out.append(Inst(f'{self.mf32} {vs(acc, 16)}, {as_(kf, 4)}, {rq(Q + 4 * ks)}, {c}', 'mfma', 8,
-                                rd=ra(kf, 4) + rqn(Q + 4 * ks), wr=rv(acc, 16),
-                                rdc=rv(acc, 16) if ks else (), pipe=32))
+                                rd=ra(kf, 4) + rqn(Q + 4 * ks) + (rv(V_SEED[X], 16) if seed else []),
+                                wr=rv(acc, 16), rdc=rv(acc, 16) if ks else (), pipe=32))
         return out
 
     def pv_sum(self, X, t):
@@ -437,7 +445,7 @@ class Gen:
             return mc
         return next(c for c in range(V_MCB[X], V_MCB[X] + 4) if c % 4 == (sreg % 4 + 2) % 4)
 
-    def exp_stream(self, X, mc, ortest=False):
+    def exp_stream(self, X, mc, ortest=False, shift=None):
         """P_X = cvt(exp2(S_X c - mc)) through the 16 rotating temporaries: fma(i) at step i,
         exp(i) at step i + EXP_LAG, cvt of pair q at step 2q + 1 + EXP_LAG + CVT_LAG (every
         consumer several instructions behind its producer; temporary i % 16 is free again before
@@ -449,9 +457,16 @@ class Gen:
         steps = []
         for i in range(32):
             e = E + i % NETMP
-            m = self.mc_reg(X, S + i, mc)
-            steps.append((i, 0, Inst(f'v_fma_f32 v{e}, v{S + i}, s{S_C}, -v{m}', 'valu', 4,
-                                     rd=[f'v{S + i}', f's{S_C}', f'v{m}'], wr=[f'v{e}'])))
+            if PRESCALE and shift is None:
+                # S^T = K Q~^T - m c already: the exp reads the accumulator
+                steps.append((i + EXP_LAG, 1, V(f'v_exp_f32 v{e}, v{S + i}', e, [S + i], kind='trans', cost=8)))
+                continue
+            if PRESCALE:    # rescale recompute: exp2(S - shift)
+                steps.append((i, 0, V(f'v_sub_f32 v{e}, v{S + i}, v{shift}', e, [S + i, shift])))
+            else:
+                m = self.mc_reg(X, S + i, mc)
+                steps.append((i, 0, Inst(f'v_fma_f32 v{e}, v{S + i}, s{S_C}, -v{m}', 'valu', 4,
+                                         rd=[f'v{S + i}', f's{S_C}', f'v{m}'], wr=[f'v{e}'])))
             steps.append((i + EXP_LAG, 1, V(f'v_exp_f32 v{e}, v{e}', e, [e], kind='trans', cost=8)))
         cvt_at = {}
         for q in range(16):
@@ -521,9 +536,16 @@ class Gen:
         touched = [f'v{mc}', f'v{mthr}'] + rv(T, 8) + ra(A_O[X], D // 2) + rqn(A_L[X]) + rv(V_ETMP, NETMP) + rv(P, 16)
         if MC_BANKS:
             touched += rv(V_MCB[X], 4)
+        if PRESCALE:
+            touched += rv(V_SEED[X], 16)
         out.append(Inst(f's_cbranch_vccnz {resc}\n{ret}:', 'br', 4, rd=['vcc'] + touched, wr=touched))
-        rb = self.rescale_block_or(X, resc, ret) if ORDET else self.rescale_block(X, resc, ret)
-        rb[-2:-2] = self.exp_stream(X, mc)       # recompute P with the new m (before the s_nop 2)
+        if PRESCALE:
+            assert ORDET
+            rb = self.rescale_block_seed(X, resc, ret)
+            rb[-2:-2] = self.exp_stream(X, mc, shift=T + 7)   # recompute P = exp2(S - shift)
+        else:
+            rb = self.rescale_block_or(X, resc, ret) if ORDET else self.rescale_block(X, resc, ret)
+            rb[-2:-2] = self.exp_stream(X, mc)       # recompute P with the new m (before the s_nop 2)
         rescue.append(rb)
         if 'nofill' in PROBE:
             out = []
@@ -665,6 +687,26 @@ class Gen:
         b.append(raw(f's_branch {ret}'))
         return b
 
+    def rescale_block_seed(self, X, resc, ret):
+        """Out-of-line rescale of the PRESCALE form: S holds s~ - m c, so its tile max T6 is the
+        excess over the current m c; lanes with T6 + delta > 0 move m c up by shift = T6 + delta
+        (P <= 2^-delta afterwards), O and the row sums are scaled by 2^-shift, the S^T seed
+        registers follow m c, and P is recomputed as exp2(S - shift) (appended by the caller)."""
+        T, mc = V_TMP[X], V_MC[X]
+        b = [label(resc), raw('s_nop 4')]
+        b += self.max_ops(X)[:-1]                   # v{T+6} = tile max of S (s~ - m c)
+        b.append(V(f'v_add_f32 v{T + 7}, {ORDET_DELTA[self.dtype]!r}, v{T + 6}', T + 7, [T + 6]))
+        b.append(V(f'v_cmp_lt_f32 vcc, 0, v{T + 7}', 'vcc', [T + 7]))
+        b.append(Inst(f'v_cndmask_b32 v{T + 7}, 0, v{T + 7}, vcc', 'valu', rd=[f'v{T + 7}', 'vcc'], wr=[f'v{T + 7}']))
+        b.append(V(f'v_sub_f32 v{T}, 0, v{T + 7}', T, [T + 7]))
+        b.append(V(f'v_exp_f32 v{T}, v{T}', T, [T], kind='trans'))
+        b.append(V(f'v_add_f32 v{mc}, v{mc}, v{T + 7}', mc, [mc, T + 7]))
+        b += [V(f'v_sub_f32 v{r}, v{r}, v{T + 7}', r, [r, T + 7]) for r in range(V_SEED[X], V_SEED[X] + 16)]
+        b += self.scale_acc(X)
+        b.append(raw('s_nop 2'))
+        b.append(raw(f's_branch {ret}'))
+        return b
+
     def scale_acc(self, X):
         """Rescale tail: m*c copies (MC_BANKS), O_X and the row sums times alpha (v{T})."""
         T, mc = V_TMP[X], V_MC[X]
@@ -757,7 +799,12 @@ class Gen:
                 x.not_before = len(qkb)
             k_lo = len(sm) * sum(m.pipe for m in qkb) // sum(m.pipe for m in mf) + 2
         if VREADS_P1:
-            side = [x for _, x in self.vreads(t)] + side
+            vr = [x for _, x in self.vreads(t)]
+            # KFIRST: K(t+1) (needed by the first MFMA of phase 2) before the V^T reads, so the
+            # counted wait at phase 2's start covers only the K reads, issued early in the phase
+            side = side + vr if KFIRST and NBK == 2 else vr + side
+            if KFIRST and NBK == 2:
+                k_lo = KFIRST_LO
         dma = [] if (last or DMA_P2) else self.dma('K', t + 1 + DIST)
         if kv_next:     # tail tile t (block tile nt - 4 + t) loads K(nt + t) = the next block's K(t)
             dma = self._dma('K', t, nxt=True)
@@ -1038,7 +1085,10 @@ def analyse(path):
         if k_l >= 0:
             younger = len(lgkm) - 1 - k_l
             in_phase = sum(1 for (_, _, ph) in lgkm if ph == phase)
-            n = min(younger, in_phase)
+            # counts reach back across phase marks only with LGKM_XPHASE (every control-flow path
+            # into the phase is enumerated, so the younger count is exact on each); the hardware
+            # counter holds at most 15
+            n = min(younger, 15) if LGKM_XPHASE else min(younger, in_phase)
             if any(o.kind == 'smem' for (o, _, _) in lgkm[:k_l + 1]):
                 n = 0
             pre.append(Inst(f's_waitcnt lgkmcnt({n})', 'wait', 0))
@@ -1380,13 +1430,17 @@ def prologue_sections(g):
           for r in range(KFB)]
     p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
     p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in (V_MTHR['A'], V_MTHR['B'], V_MC['A'], V_MC['B'])]
+    if PRESCALE:
+        p += [V(f'v_mov_b32 v{r}, {-SEED0!r}', r, []) for r in (V_MC['A'], V_MC['B'])]
+        p += [V(f'v_mov_b32 v{r}, {SEED0!r}', r, []) for X in BLOCKS for r in range(V_SEED[X], V_SEED[X] + 16)]
     if MC_BANKS:
         p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in range(V_MCB['A'], V_MCB['B'] + 4)]
     p.append(sec('start'))
     p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
     # (8 waves: phase 0 reads K2 as well: K0 K1 V0 K2 landed, all but the 3 youngest pieces)
-    p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else pieces_wait()})'), raw('s_barrier')]
+    p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else pieces_wait()})')]
+    p += q_prescale(g) + [raw('s_barrier')]
     p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
     # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
     p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
@@ -1398,6 +1452,37 @@ def prologue_sections(g):
                   label('.Lprio_done')]
     p += [raw('s_nop 7'), raw('s_nop 3')]
     return p
+
+
+def q_prescale(g):
+    """PRESCALE: Q~ = rne16(Q c) in place (AGPR fragments of every block, after they landed):
+    per register the two 16-bit halves widened to fp32, multiplied by c, packed back. The
+    per-register chains run 8 at a time, interleaved, so no op waits on its predecessor."""
+    if not PRESCALE:
+        return []
+    chains = []
+    k = 0
+    for X in BLOCKS:
+        for r in range(4 * NKS):
+            q = A_Q[X] + r
+            a, lo, hi = (V_S['A'] + (k % 8) * 4 + j for j in range(3))   # S registers: free before QK_A(0)
+            c = [Inst(f'v_accvgpr_read_b32 v{a}, a{q}', 'accr', rd=[f'a{q}'], wr=[f'v{a}'])]
+            if g.dtype == 'bf16':
+                c += [V(f'v_lshlrev_b32 v{lo}, 16, v{a}', lo, [a]), V(f'v_and_b32 v{hi}, 0xffff0000, v{a}', hi, [a])]
+            else:
+                c += [V(f'v_cvt_f32_f16 v{lo}, v{a}', lo, [a]), V(f'v_lshrrev_b32 v{hi}, 16, v{a}', hi, [a]),
+                      V(f'v_cvt_f32_f16 v{hi}, v{hi}', hi, [hi])]
+            c += [V(f'v_mul_f32 v{lo}, s{S_C}, v{lo}', lo, [lo]), V(f'v_mul_f32 v{hi}, s{S_C}, v{hi}', hi, [hi]),
+                  V(f'{g.cvt} v{a}, v{lo}, v{hi}', a, [lo, hi]),
+                  Inst(f'v_accvgpr_write_b32 a{q}, v{a}', 'accw', rd=[f'v{a}'], wr=[f'a{q}'])]
+            chains.append(c)
+            k += 1
+    res = []
+    for base in range(0, len(chains), 8):
+        grp = chains[base:base + 8]
+        for j in range(max(len(c) for c in grp)):
+            res += [c[j] for c in grp if j < len(c)]
+    return res
 
 
 def split_sections(lst):
@@ -1443,6 +1528,23 @@ def tail_blocks(g, rescue):
     b += [mark()] + g.epilogue('B')
     b += [S('s_mov_b32 s101, 2'), raw('s_branch .Lseam')]
     return b
+
+
+def set_prescale(on):
+    """PRESCALE on/off (D = 64, 4 waves): the seed registers raise the VGPR count."""
+    global PRESCALE, NVGPR
+    if on:
+        assert D == 64 and NWAVES == 4 and ORDET
+        NVGPR = max(NVGPR, V_SEED['B'] + 16)
+    PRESCALE = on
+
+
+def product_prescale(dtype, hd, waves):
+    """The shipped setting (build.py, tests): PRESCALE for the D = 64 four-wave forms."""
+    return hd == 64 and waves == 4 and PRESCALE_PRODUCT.get(dtype, False)
+
+
+PRESCALE_PRODUCT = {'bf16': False, 'f16': False}
 
 
 def set_persist(on):
@@ -1598,7 +1700,9 @@ STAMP_V = 168
 
 
 def stamp(lo):
-    return [raw('s_memrealtime s[96:97]'), raw('s_waitcnt lgkmcnt(0)'),
+    # 'stampcyc': shader-clock cycles (s_memtime) instead of the 100 MHz real-time counter
+    clk = 's_memtime' if 'stampcyc' in PROBE else 's_memrealtime'
+    return [raw(f'{clk} s[96:97]'), raw('s_waitcnt lgkmcnt(0)'),
             raw(f'v_mov_b32 v{lo}, s96'), raw(f'v_mov_b32 v{lo + 1}, s97')]
 
 
@@ -1871,6 +1975,9 @@ def main():
     ap.add_argument('--ordet', type=int, default=None)
     ap.add_argument('--lag', default=None, help='EXP_LAG,CVT_LAG')
     ap.add_argument('--mcbanks', type=int, default=None)
+    ap.add_argument('--kfirst', type=int, default=None, help='K(t+1) reads first in phase 1 (value: first position)')
+    ap.add_argument('--prescale', type=int, default=None, help='Q pre-scaled by c, S^T seeded with -m c (D = 64, 4 waves)')
+    ap.add_argument('--xphase', type=int, default=None, help='counted lgkmcnt waits across phase marks')
     args = ap.parse_args()
     global DUMP
     if args.dump:
@@ -1897,16 +2004,23 @@ def main():
         EXP_LAG, CVT_LAG = (int(x) for x in args.lag.split(','))
     if args.mcbanks is not None:
         MC_BANKS = bool(args.mcbanks)
+    global KFIRST, KFIRST_LO, LGKM_XPHASE, PRESCALE
+    prescale = product_prescale(args.dtype, args.hd, args.waves) if args.prescale is None else bool(args.prescale)
+    if args.kfirst is not None:
+        KFIRST, KFIRST_LO = args.kfirst > 0, max(0, args.kfirst)
+    if args.xphase is not None:
+        LGKM_XPHASE = bool(args.xphase)
     global PRIO4
     if args.prio4 is not None:
         PRIO4 = bool(args.prio4)
     set_persist(bool(args.persist))
+    set_prescale(prescale)
     if MC_BANKS:
         NVGPR = max(NVGPR, V_MCB['B'] + 4)
     global KARG_BYTES
     if 'stamps' in PROBE:
-        assert args.hd == 64 and NVGPR <= STAMP_V
-        NVGPR = STAMP_V + 16
+        assert args.hd == 64 and not PERSIST and (not PRESCALE or V_SEED['A'] >= STAMP_V + 16)
+        NVGPR = max(NVGPR, STAMP_V + 16)
         KARG_BYTES += 8
     g = Gen(args.dtype)
     blocks, n = build(g)

@@ -75,6 +75,14 @@ const char *fa_last_error(void) { return g_last_error.c_str(); }
 
 const char *fa_version(void) { return "fa_hip 0.1.0 (gfx950)"; }
 
+const char *fa_fwd_kernel_name(const FaFwdArgs *a) {
+    if (a == nullptr || a->head_dim <= 0 || a->head_dim > 128 || a->batch <= 0 || a->nheads <= 0) return nullptr;
+    if (fa::fwd_asm_eligible(*a, FaBlockMask{nullptr, 0, 0, 0})) return fa::asm_kernel_name(*a);
+    const int t = a->head_dim <= 32 ? 32 : a->head_dim <= 64 ? 64 : 128;
+    return t == 32 ? "fa_fwd_kernel (HIP, D=32 tile)" : t == 64 ? "fa_fwd_kernel (HIP, D=64 tile)"
+                                                          : "fa_fwd_kernel (HIP, D=128 tile)";
+}
+
 int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {
     switch (what) {
         case FA_QUERY_BWD_WORKSPACE: return a * b * c * (int64_t)sizeof(float);

@@ -200,14 +200,33 @@ static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
     return nwg > (uint32_t)g ? g : 0;
 }
 
+// The code object launch_fwd_asm runs for these arguments (form index of kNumFns / 2) and the
+// persistent grid (0: one workgroup per block).
+static int asm_form(const FaFwdArgs &a, int *pgrid) {
+    const bool w8 = use_w8(a);
+    const uint32_t nqb0 = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
+    *pgrid = w8 ? 0 : persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
+    const bool d128 = a.head_dim > 64;
+    return w8 ? 2 : *pgrid ? (d128 ? 4 : 3) : (d128 ? 1 : 0);
+}
+
+const char *asm_kernel_name(const FaFwdArgs &a) {
+    static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
+                                               "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
+                                               "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
+                                               "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
+                                               "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm"};
+    int pgrid = 0;
+    return names[2 * asm_form(a, &pgrid) + (a.dtype == FA_DTYPE_BF16 ? 0 : 1)];
+}
+
 hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavailable) {
     hipFunction_t fn = nullptr;
     *unavailable = false;
     const bool w8 = use_w8(a);
-    const uint32_t nqb0 = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
-    const int pgrid = w8 ? 0 : persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
-    const bool d128 = a.head_dim > 64;
-    hipError_t e = get_function(a.dtype, w8 ? 2 : pgrid ? (d128 ? 4 : 3) : (d128 ? 1 : 0), &fn);
+    int pgrid = 0;
+    const int form = asm_form(a, &pgrid);
+    hipError_t e = get_function(a.dtype, form, &fn);
     if (e != hipSuccess) {
         (void)hipGetLastError();   // the load error is not the caller's launch error
         *unavailable = true;

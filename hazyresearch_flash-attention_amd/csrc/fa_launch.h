@@ -38,6 +38,8 @@ hipError_t launch_zero_seq_rows(void *base, const int32_t *cu, int64_t row_strid
                                 int nheads, int head_dim, int max_seqlen, hipStream_t s);
 // hand-scheduled assembly forward (fa_asm.cpp, csrc/asm/gen_fwd.py)
 bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm);
+// symbol name of the code object launch_fwd_asm would run for a
+const char *asm_kernel_name(const FaFwdArgs &a);
 // *unavailable is set (and hipSuccess returned, nothing launched) when the device's code objects
 // could not be loaded: the caller then runs the HIP kernels (fa_asm.cpp load_all).
 hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavailable);

@@ -148,6 +148,8 @@ def lib():
         h.fa_last_error.restype = ctypes.c_char_p
         h.fa_version.argtypes = []
         h.fa_version.restype = ctypes.c_char_p
+        h.fa_fwd_kernel_name.argtypes = [ctypes.POINTER(FaFwdArgs)]
+        h.fa_fwd_kernel_name.restype = ctypes.c_char_p
         if h.fa_query(FA_QUERY_FWD_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaFwdArgs):
             raise ImportError("FaFwdArgs layout mismatch between fa_hip.h and flash_attn_hip.py")
         if h.fa_query(FA_QUERY_BWD_ARGS_SIZE, 0, 0, 0) != ctypes.sizeof(FaBwdArgs):
@@ -610,3 +612,21 @@ def rotary(x, y, cos, sin, shape, x_strides, y_strides, nrot, inverse):
     if rc != 0:
         _raise(rc, "fa_rotary")
     return y
+
+
+def fwd_kernel_name(batch, nheads, head_dim, max_seqlen_q, max_seqlen_k, dtype=torch.bfloat16, causal=False,
+                    p_dropout=0.0, row_elems=None, impl=FA_IMPL_AUTO):
+    """Name of the GPU kernel fa_fwd launches for a dense forward of this shape (as rocprofv3 shows it;
+    include/fa_hip.h fa_fwd_kernel_name). row_elems: the q/k/v/o row stride in elements (default
+    nheads * head_dim, the unpadded layout)."""
+    a = FaFwdArgs()
+    rs = nheads * head_dim if row_elems is None else row_elems
+    a.q_row_stride = a.k_row_stride = a.v_row_stride = a.o_row_stride = rs
+    a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = head_dim
+    a.batch, a.nheads, a.head_dim = batch, nheads, head_dim
+    a.max_seqlen_q, a.max_seqlen_k = max_seqlen_q, max_seqlen_k
+    a.lse_stride = max((max_seqlen_q + 15) // 16 * 16, 16)
+    a.softmax_scale, a.p_dropout = head_dim ** -0.5, p_dropout
+    a.is_causal, a.dtype, a.impl = int(causal), _dtype_code(dtype), impl
+    name = lib().fa_fwd_kernel_name(ctypes.byref(a))
+    return None if name is None else name.decode()

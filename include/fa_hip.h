@@ -25,7 +25,7 @@
  *    no fused rotary; the persistent form for
  *    non-causal grids with more blocks than CUs (fa_asm.cpp fwd_asm_eligible / persistent_grid_for).
  *    FaFwdArgs.impl selects a form or the HIP kernels.)
- *   fa_query, fa_last_error, fa_version: host helpers (no reference counterpart; the reference
+ *   fa_query, fa_last_error, fa_version, fa_fwd_kernel_name: host helpers (no reference counterpart; the reference
  *                                                  raised through TORCH_CHECK / exit(1),
  *                                                  fmha_api.cpp:131-170, fmha_utils.h:36-48)
  *
@@ -240,6 +240,11 @@ const char *fa_last_error(void);
 
 /* Library version string. */
 const char *fa_version(void);
+
+/* Name of the GPU kernel fa_fwd would launch for these arguments (e.g. "fa_fwd_d64p_bf16_asm"), as
+ * it appears in a rocprofv3 kernel trace; NULL if the arguments are invalid. Launches nothing
+ * (host helper, like fa_query; used by bench.py to name the kernel its roofline measures). */
+const char *fa_fwd_kernel_name(const FaFwdArgs *args);
 
 #ifdef __cplusplus
 }

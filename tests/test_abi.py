@@ -19,9 +19,9 @@ def _declared_functions():
 
 
 def test_header_declares_the_entry_points():
-    assert _declared_functions() == ["fa_bwd", "fa_bwd_block", "fa_fwd", "fa_fwd_block", "fa_index_add_first_axis",
-                                     "fa_index_first_axis", "fa_index_put_first_axis", "fa_last_error", "fa_query",
-                                     "fa_rotary", "fa_version"]
+    assert _declared_functions() == ["fa_bwd", "fa_bwd_block", "fa_fwd", "fa_fwd_block", "fa_fwd_kernel_name",
+                                     "fa_index_add_first_axis", "fa_index_first_axis", "fa_index_put_first_axis", "fa_last_error",
+                                     "fa_query", "fa_rotary", "fa_version"]
 
 
 def test_library_exports_every_declared_symbol():

@@ -24,20 +24,27 @@ from oracle.attention_ref import attention_ref  # noqa: E402
 _TXT = {}
 
 
-def _kernel(dtype, hd=64, waves=4, persist=False):
-    if (dtype, hd, waves, persist) not in _TXT:
+def _kernel(dtype, hd=64, waves=4, persist=False, prescale=None):
+    """prescale: None = the product setting of build.py for this form (gen_fwd.product_prescale)."""
+    if prescale is None:
+        prescale = gen_fwd.product_prescale(dtype, hd, waves)
+    key = (dtype, hd, waves, persist, prescale)
+    if key not in _TXT:
         gen_fwd.configure(hd, waves)
         try:
             gen_fwd.set_persist(persist)
+            gen_fwd.set_prescale(prescale)
             g = gen_fwd.Gen(dtype)
             blocks, _ = gen_fwd.build(g)
-            _TXT[(dtype, hd, waves, persist)] = gen_fwd.emit(g, blocks)
+            _TXT[key] = gen_fwd.emit(g, blocks)
         finally:
+            gen_fwd.set_prescale(False)
+            gen_fwd.set_persist(False)
             gen_fwd.configure(64)
-    return _TXT[(dtype, hd, waves, persist)]
+    return _TXT[key]
 
 
-def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4, grid=None):
+def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4, grid=None, prescale=None):
     """grid: the persistent form's workgroup count (each walks blocks L, L + grid, ...)."""
     rng = np.random.default_rng(seed)
     cv = asm_sim.bf16_bits if dtype == "bf16" else asm_sim.f16_bits
@@ -70,7 +77,7 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4,
     if grid:
         karg += struct.pack("<2I", grid, 0)
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
-    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64 if D > 32 else 32, waves, bool(grid)), dtype).run(
+    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64 if D > 32 else 32, waves, bool(grid), prescale), dtype).run(
         (grid, 1, 1) if grid else (nqb, H, B), pa, mem)
     o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
     lse = mem.get(pl).view(np.float32).reshape(B, H, lse_stride)
@@ -95,6 +102,12 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4,
                 s = s.masked_fill(cmask, float("-inf"))
             ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), vf[sk].double()).float()
             base = 4e-3
+            if prescale:
+                # the PyTorch low-precision baseline at this scale: scores rounded to the input type
+                # (as attention_ref(upcast=False) rounds its einsum output), softmax, P V
+                s_lo = s.to(tdt).double()
+                lo = torch.einsum("hqk,khd->qhd", torch.softmax(s_lo, -1).to(tdt).double(), vf[sk].double()).float()
+                base = max(base, (lo - ref).abs().max().item())
         else:
             lo = attention_ref(*(x.to(tdt) for x in args), upcast=False, causal=causal)[0][0].float()
             base = (lo - ref).abs().max().item()
@@ -104,8 +117,13 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4,
             s = s.masked_fill(cmask, float("-inf"))
         ref_lse = torch.logsumexp(s, -1).numpy()
         # the row sums cover the 16-bit-rounded P (what multiplies V): up to 2^-8 relative in the
-        # sum, so the LSE is within 4e-3
-        assert np.abs(lse[b, :, :lens_q[b]] - ref_lse).max() < 4e-3
+        # sum, so the LSE is within 4e-3; the PRESCALE form's scores carry the
+        # rounding of Q c to the input type: its bound is twice the LSE error of scores rounded
+        # to the input type (the low-precision baseline above)
+        tol = 4e-3
+        if prescale:
+            tol = max(tol, 2 * np.abs(torch.logsumexp(s.to(tdt).double(), -1).numpy() - ref_lse).max())
+        assert np.abs(lse[b, :, :lens_q[b]] - ref_lse).max() < tol
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
@@ -222,3 +240,17 @@ def test_asm_forward_d32_in_simulator(lens_q, lens_k, H, D, dtype):
 def test_asm_forward_d32_causal_and_persistent_in_simulator():
     _run([300], [300], 1, 32, "bf16", causal=True)
     _run([300, 200], [512, 256], 2, 24, "bf16", grid=2)
+
+
+@pytest.mark.parametrize("lens_q,lens_k,H,D,grid,dtype,causal,scale", [
+    ([130], [200], 1, 64, None, "bf16", False, None),       # one-block form: 3 full tiles + a masked one
+    ([70], [700], 1, 64, None, "f16", False, None),         # 11 tiles, fp16 (rescale delta 2)
+    ([40, 64], [0, 65], 1, 48, None, "bf16", False, None),  # empty key set, head_dim < 64
+    ([300], [300], 1, 64, None, "bf16", True, None),        # causal band
+    ([70], [300], 1, 64, None, "bf16", False, 3.0),         # forced rescales past tile 0
+    ([300, 200], [512, 256], 2, 64, 1, "bf16", False, None),  # persistent: K/V tail, next-Q copy at the seam
+    ([300, 100], [512, 320], 2, 64, 3, "f16", False, None),   # persistent: tails, empty q-block, fp16
+])
+def test_asm_forward_prescaled_in_simulator(lens_q, lens_k, H, D, grid, dtype, causal, scale):
+    """The PRESCALE form (Q~ = Q c rounded once per block, S^T seeded with -m c, softmax exp2(S))."""
+    _run(lens_q, lens_k, H, D, dtype, scale=scale, causal=causal, grid=grid, prescale=True)

@@ -361,7 +361,7 @@ class Sim:
             if kind.endswith('f32'):
                 p, q = self.fread(w, x), self.fread(w, y)
                 c = kind[:-4]
-                res = {'gt': p > q, 'nlg': ~((p < q) | (p > q))}[c]
+                res = {'gt': p > q, 'lt': p < q, 'nlg': ~((p < q) | (p > q))}[c]
             elif kind.endswith('i32'):
                 p, q = self.vread(w, x).view(np.int32), self.vread(w, y).view(np.int32)
                 res = {'lt': p < q, 'gt': p > q, 'eq': p == q}[kind[:-4]]
@@ -439,6 +439,8 @@ class Sim:
                 r = (f[0] + f[1]).astype(np.float32)
             elif op == 'v_sub_f32':
                 r = (f[0] - f[1]).astype(np.float32)
+            elif op == 'v_cvt_f32_f16':
+                r = (src[0] & 0xFFFF).astype(np.uint16).view(np.float16).astype(np.float32)
             elif op == 'v_exp_f32':
                 r = np.exp2(f[0]).astype(np.float32)
             elif op == 'v_log_f32':

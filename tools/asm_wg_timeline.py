@@ -25,9 +25,9 @@ GEN = os.path.join(ROOT, "hazyresearch_flash-attention_amd", "csrc", "asm", "gen
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-def build(out_dir):
-    s = os.path.join(out_dir, "stamps.s")
-    subprocess.check_call([sys.executable, GEN, "--out", s, "--probe", "stamps"])
+def build(out_dir, cyc=False):
+    s = os.path.join(out_dir, "stampcyc.s" if cyc else "stamps.s")
+    subprocess.check_call([sys.executable, GEN, "--out", s, "--probe", "stamps,stampcyc" if cyc else "stamps"])
     subprocess.check_call([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
                            s, "-o", s[:-2] + ".o"])
     subprocess.check_call([f"{LLVM}/ld.lld", "-shared", s[:-2] + ".o", "-o", s[:-2] + ".hsaco"])
@@ -39,10 +39,12 @@ def main():
     ap.add_argument("--shape", default="8,12,2048,2048")
     ap.add_argument("--causal", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cycles", action="store_true",
+                    help="stamp with s_memtime (shader cycles) instead of s_memrealtime; durations in kcycles")
     args = ap.parse_args()
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)
-    img = build(out_dir)
+    img = build(out_dir, args.cycles)
     import torch
     B, H, Sq, Sk = (int(x) for x in args.shape.split(","))
     D = 64
@@ -108,7 +110,7 @@ def main():
     hwid, xcc = rec[:, 6], rec[:, 7]
     wg = rec[:, 8] + nqb * (rec[:, 9] + H * rec[:, 10])
     base = t0.min()
-    us = lambda x: (x - base) * 0.01
+    us = (lambda x: (x - base) * 1e-3) if args.cycles else (lambda x: (x - base) * 0.01)
     wgs = defaultdict(list)
     for i in range(n):
         wgs[int(wg[i])].append(i)
@@ -131,7 +133,8 @@ def main():
         for a, b in zip(rs, rs[1:]):
             gaps.append(b["start"] - a["end"])
     med = lambda xs: float(np.median(xs))
-    res = {"shape": args.shape, "causal": args.causal, "event_us": round(ev_us, 2),
+    res = {"shape": args.shape, "causal": args.causal, "unit": "kcycles" if args.cycles else "us",
+           "event_us": round(ev_us, 2),
            "stamp_span_us": round(max(r["end"] for r in rows), 2), "cus": len(percu),
            "wg_per_cu": [min(counts), max(counts)],
            "prologue_us_med": round(med([r["pro"] for r in rows]), 3),
