@@ -1442,6 +1442,7 @@ def prologue_sections(g):
     p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else pieces_wait()})')]
     p += q_prescale(g) + [raw('s_barrier')]
     p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
+    p += pstamp(PS_V + 4)
     # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
     p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
     if NWAVES == 8:
@@ -1521,7 +1522,7 @@ def tail_blocks(g, rescue):
     for t in range(3):
         b += g.phase1(t, rescue=rescue, kv_next=True) + g.phase2(t, rescue=rescue, kv_next=True)
         b += [raw(f's_waitcnt vmcnt({tile_vmcnt()})'), raw('s_barrier'), S(f's_add_u32 s{S_J}, s{S_J}, 1')]
-    b += nvrel_insts()
+    b += pstamp(PS_V + 6) + nvrel_insts()
     b += g.phase1(3, masked=True, last=True, rescue=rescue, kv_next=True)
     b += g.phase2(3, masked=True, last=True, rescue=rescue, kv_next=True)
     b += [mark()] + place(g.pv_sum('B', 3)[0], g.epilogue('A'))
@@ -1568,7 +1569,9 @@ def set_persist(on):
 def prologue_persist(g):
     """Blocks of the persistent prologue: (pro_a, pb1, qcopy, qload, pb2)."""
     sc = split_sections(prologue_sections(g))
-    pro_a = sc['args'] + [Inst('s_load_dword s100, s[0:1], 0xa8', 'smem', 2, wr=['s100']),
+    ps_ptr = [raw(f's_load_dwordx2 s[96:97], s[0:1], {KARG_BYTES - 8:#x}'), raw('s_waitcnt lgkmcnt(0)'),
+              raw(f'v_mov_b32 v{PS_V}, s96'), raw(f'v_mov_b32 v{PS_V + 1}, s97')] if 'pstamps' in PROBE else []
+    pro_a = sc['args'] + ps_ptr + [Inst('s_load_dword s100, s[0:1], 0xa8', 'smem', 2, wr=['s100']),
                           raw('s_waitcnt lgkmcnt(0)'),
                           S('s_mov_b32 s99, s2'), S('s_mov_b32 s101, 0'), S('s_mov_b32 s98, 0'),
                           V(f'v_mov_b32 v{V_TID}, v0', V_TID, [0])]
@@ -1581,7 +1584,7 @@ def prologue_persist(g):
     nxt += make_desc(S_NQD, 40, 76, 62, 54, 55, 77)
     lanes_t = [V(f'v_and_b32 v16, 31, v{V_TID}', 16, [V_TID]), V(f'v_bfe_u32 v17, v{V_TID}, 5, 1', 17, [V_TID]),
                V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
-    pb1 = [label('.Lblock')] + nxt + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + \
+    pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + nxt + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + \
         sc['state'] + lanes_t + \
         sc['rows'] + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
     qcopy = [Inst(f'v_accvgpr_write_b32 a{A_Q[X] + r}, v{V_QN + 16 * xi + r}', 'accw',
@@ -1732,6 +1735,33 @@ def stamp_exit():
         raw('s_waitcnt vmcnt(0)')]
 
 
+# 'pstamps' probe (tools/asm_pstamps.py, persistent D = 64 form): per (block, wave) four s_memtime
+# stamps -- block entry (.Lblock), loop start (after the start barrier), last-tile entry, seam --
+# stored by lane 0 as a 32-byte record at [ptr + 32 (4 L + wave)]; ptr = the 8 kernel-argument bytes
+# after KARG_BYTES - 8, kept in v244:245 (v244..v255 are free in the persistent form).
+PS_V = 244
+
+
+def pstamp(lo):
+    if 'pstamps' not in PROBE:
+        return []
+    return [raw('s_memtime s[96:97]'), raw('s_waitcnt lgkmcnt(0)'), raw(f'v_mov_b32 v{lo}, s96'),
+            raw(f'v_mov_b32 v{lo + 1}, s97')]
+
+
+def pstamp_store():
+    if 'pstamps' not in PROBE:
+        return []
+    b = PS_V
+    return pstamp(b + 8) + [
+        raw(f's_lshl_b32 s96, s{S_L}, 2'), raw(f's_add_u32 s96, s96, s{S_WAVE}'), raw('s_lshl_b32 s96, s96, 5'),
+        raw(f'v_add_co_u32 v{b + 10}, vcc, s96, v{b}'), raw(f'v_addc_co_u32 v{b + 11}, vcc, 0, v{b + 1}, vcc'),
+        raw('s_mov_b64 s[96:97], exec'), raw('s_mov_b64 exec, 1'), raw('s_nop 1'),
+        raw(f'global_store_dwordx4 v[{b + 10}:{b + 11}], v[{b + 2}:{b + 5}], off'),
+        raw(f'global_store_dwordx4 v[{b + 10}:{b + 11}], v[{b + 6}:{b + 9}], off offset:16'),
+        raw('s_mov_b64 exec, s[96:97]')]
+
+
 def nvrel_insts():
     """Per-block key limits of a masked tile: NVREL_X = ROW1_X - 64 j."""
     return [S(f's_lshl_b32 s96, s{S_J}, 6')] + \
@@ -1773,7 +1803,7 @@ def masked_tile(g, t, rescue):
 def last_tile(g, t, rescue):
     """Tile t = nt - 1 (position t of the unrolled loop): masked softmax of both blocks, no
     next-tile reads or DMA, then P.V of block B and the two epilogues."""
-    b = [label(f'.Llast{t}')] + (stamp(STAMP_V + 2) if 'stamps' in PROBE else []) + nvrel_insts()
+    b = [label(f'.Llast{t}')] + (stamp(STAMP_V + 2) if 'stamps' in PROBE else []) + pstamp(PS_V + 6) + nvrel_insts()
     b += tile_phases(g, t, masked=True, last=True, rescue=rescue)
     if NWAVES == 8:
         b += [mark()] + place(g.pv_sum(par(t), t)[0], [])
@@ -1832,7 +1862,7 @@ def build(g):
     end = [label('.Lend'), raw('s_endpgm')]
     if PERSIST:
         # .Lend (q-block past its sequence: nothing prefetched) and .Lseam (after a block): next block
-        end = [label('.Lend'), S(f's_mov_b32 s{S_QPF}, 0'), label('.Lseam'),
+        end = [label('.Lend'), S(f's_mov_b32 s{S_QPF}, 0'), label('.Lseam')] + pstamp_store() + [
                S(f's_add_u32 s{S_L}, s{S_L}, s{S_G}'), S(f's_cmp_ge_u32 s{S_L}, s71'), raw('s_cbranch_scc1 .Ldone'),
                raw('s_barrier'), raw('s_branch .Lblock')]
         done = [label('.Ldone'), raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
@@ -2018,6 +2048,10 @@ def main():
     if MC_BANKS:
         NVGPR = max(NVGPR, V_MCB['B'] + 4)
     global KARG_BYTES
+    if 'pstamps' in PROBE:
+        assert args.hd == 64 and PERSIST and NVGPR <= PS_V
+        NVGPR = 256
+        KARG_BYTES += 8
     if 'stamps' in PROBE:
         assert args.hd == 64 and not PERSIST and (not PRESCALE or V_SEED['A'] >= STAMP_V + 16)
         NVGPR = max(NVGPR, STAMP_V + 16)

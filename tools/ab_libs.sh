@@ -7,8 +7,8 @@ CFGS=$1; MODES=$2; shift 2
 L=$GRAFT_REPO_ROOT/hazyresearch_flash-attention_amd/flash_attn
 for r in 1 2; do
 for c in $CFGS; do for m in $MODES; do
-  timeout -k 10 120 python tools/tiles_r03.py --cfg $c --mode $m --launches 100 >> gpurun_out/ab_libs.txt 2>&1
+  timeout -k 10 120 python tools/tiles_run.py --cfg $c --mode $m --launches 100 >> gpurun_out/ab_libs.txt 2>&1
   for t in "$@"; do
-    FA_HIP_LIB=$L/libfa_hip_$t.so timeout -k 10 120 python tools/tiles_r03.py --cfg $c --mode $m --launches 100 | sed "s/\"cfg\"/\"lib\": \"$t\", \"cfg\"/" >> gpurun_out/ab_libs.txt 2>&1
+    FA_HIP_LIB=$L/libfa_hip_$t.so timeout -k 10 120 python tools/tiles_run.py --cfg $c --mode $m --launches 100 | sed "s/\"cfg\"/\"lib\": \"$t\", \"cfg\"/" >> gpurun_out/ab_libs.txt 2>&1
   done
 done; done; done

@@ -1,13 +1,13 @@
 """Steady-state driver of one configuration for the per-tile roofline (profiles/r03_tiles_roofline.json).
 
-    python tools/tiles_r03.py --cfg D64 --mode fwd [--launches 200] [--warm 0.3]
+    python tools/tiles_run.py --cfg D64 --mode fwd [--launches 200] [--warm 0.3]
 
 Runs the product binding (flash_attn_hip.fwd / .bwd, the calls flash_attn_interface makes) for
 one mode only: `fwd` repeats the forward; `bwd` runs one forward, then repeats the backward on
 its saved outputs (no forward in the timed loop). A warm-up of at least `--warm` seconds comes
 first (clock ramp), then `--launches` calls bracketed by HIP events on the binding's stream; one
 JSON line reports the event time per call. Under rocprofv3 the last `--launches` dispatches of
-each kernel are the timed ones (tools/tiles_r03_summary.py takes exactly those).
+each kernel are the timed ones (tools/tiles_summary.py takes exactly those).
 """
 import argparse
 import json
