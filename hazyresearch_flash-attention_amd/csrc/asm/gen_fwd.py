@@ -68,9 +68,9 @@ PRESCALE = False       # Q pre-multiplied by c (rounded to the 16-bit type once 
 #                        with -m c (16 registers per block): the softmax is exp2(S), no per-element fma
 SEED0 = 4096.0         # initial -m c: every tile 0 fires the rescale unless all its scores are < -3968
 V_SEED = {'A': 212, 'B': 228}   # PRESCALE: -m c broadcast over the 16 registers of an S^T tile
-KFIRST = False         # phase 1: K(t+1) fragment reads ahead of the V^T reads (D = 64)
+KFIRST = True          # phase 1: K(t+1) fragment reads ahead of the V^T reads (D = 64)
 KFIRST_LO = 2          # softmax-stream position of the first K read with KFIRST
-LGKM_XPHASE = False    # counted lgkmcnt waits may count LDS reads of the previous phase
+LGKM_XPHASE = True     # counted lgkmcnt waits may count LDS reads of the previous phase
 
 
 def set_geometry(r, dist):
@@ -1157,11 +1157,10 @@ def fix_paths(paths, max_iter=400):
     total = 0
     for _ in range(max_iter):
         changed = 0
-        for mk in paths:
+        for mk in paths:      # every path once per sweep (each rebuilt after the previous insertions)
             ins = analyse(mk())
             if ins:
-                changed = apply_insertions(ins)
-                break
+                changed += apply_insertions(ins)
         total += changed
         if not changed:
             return total
@@ -1545,7 +1544,7 @@ def product_prescale(dtype, hd, waves):
     return hd == 64 and waves == 4 and PRESCALE_PRODUCT.get(dtype, False)
 
 
-PRESCALE_PRODUCT = {'bf16': False, 'f16': False}
+PRESCALE_PRODUCT = {'bf16': True, 'f16': False}
 
 
 def set_persist(on):
@@ -1876,13 +1875,21 @@ def build(g):
     if PERSIST:
         first = lambda: refs(pro_a) + refs(pb1) + refs(qload) + refs(pb2)
         qsel = qcopy if PERSIST_Q else qload
-        nxt = lambda: refs(end) + refs(pb1) + refs(qsel) + refs(pb2)
+        # a finished block reaches the next one at .Lseam (the .Lend entry above it drains vmcnt, .Lseam does not)
+        iseam = next(i for i, x in enumerate(end) if x.kind == 'label' and x.txt.startswith('.Lseam'))
+        seam = lambda: [(end, k) for k in range(iseam, len(end))]
+        nxt = lambda: seam() + refs(pb1) + refs(qsel) + refs(pb2)
         lend = next(i for i, x in enumerate(pb1) if x.txt.endswith('.Lend'))
         paths.append(lambda: first() + seq(tiles) + seq(tiles))
         for t in range(U):
             paths.append(lambda t=t: first() + seq(tiles) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
             paths.append(lambda t=t: first() + seq(tiles) + seq(masks) + seq(masks[:t]) + refs(lasts[t]) + nxt() +
                          seq(tiles))
+            # the masked loop (causal band / last tile) entered after only t main tiles of the block's first
+            # round, and its last tile reached directly (blocks of fewer than U tiles)
+            paths.append(lambda t=t: first() + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
+            paths.append(lambda t=t: first() + seq(tiles[:t]) + [(masks[t], k) for k in range(3)] + refs(lasts[t]) +
+                         nxt() + seq(tiles))
         paths.append(lambda: first() + refs(empty) + nxt() + seq(tiles))
         paths.append(lambda: refs(pro_a) + [(pb1, k) for k in range(lend + 1)] + refs(end) + refs(pb1) + refs(qload) +
                      refs(pb2) + seq(tiles))
@@ -1890,7 +1897,11 @@ def build(g):
         ikv = next(i for i, x in enumerate(pb2) if x.txt.endswith('.Lkvpf'))
         for_tail = lambda: first() + seq(tiles) + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
         paths.append(lambda: for_tail() + nxt_from_tail() + seq(tiles) + seq(tiles))
-        nxt_from_tail = lambda: refs(end) + refs(pb1) + refs(qsel) + [(pb2, k) for k in range(ikv + 1)] + refs(pb2k)
+        # a block of exactly 4 tiles enters the tail at its first tile
+        tail_now = lambda: first() + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
+        paths.append(lambda: tail_now() + nxt_from_tail() + seq(tiles) + seq(tiles))
+        paths.append(lambda: for_tail() + nxt_from_tail() + [(tiles[0], k) for k in range(itail + 1)] + refs(tail))
+        nxt_from_tail = lambda: seam() + refs(pb1) + refs(qsel) + [(pb2, k) for k in range(ikv + 1)] + refs(pb2k)
     else:
         paths.append(lambda: refs(pro) + seq(tiles) + seq(tiles))
         for t in range(U):
@@ -1898,6 +1909,10 @@ def build(g):
             paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
             # masked loop -> last tile at position t
             paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(masks) + seq(masks[:t]) + refs(lasts[t]))
+            # the masked loop entered after only t main tiles (causal band from tile t < U), and its last
+            # tile reached directly (fewer than U tiles)
+            paths.append(lambda t=t: refs(pro) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
+            paths.append(lambda t=t: refs(pro) + seq(tiles[:t]) + [(masks[t], k) for k in range(3)] + refs(lasts[t]))
         paths.append(lambda: refs(pro) + refs(empty))
     # rescale blocks entered from their branch: the 40 instructions before it, the block, the rest
     def resc_path(rb):

@@ -77,7 +77,10 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4,
     if grid:
         karg += struct.pack("<2I", grid, 0)
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
-    asm_sim.Sim(_kernel(dtype, 128 if D > 64 else 64 if D > 32 else 32, waves, bool(grid), prescale), dtype).run(
+    hd = 128 if D > 64 else 64 if D > 32 else 32
+    if prescale is None:
+        prescale = gen_fwd.product_prescale(dtype, hd, waves)
+    asm_sim.Sim(_kernel(dtype, hd, waves, bool(grid), prescale), dtype).run(
         (grid, 1, 1) if grid else (nqb, H, B), pa, mem)
     o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
     lse = mem.get(pl).view(np.float32).reshape(B, H, lse_stride)
@@ -254,3 +257,58 @@ def test_asm_forward_d32_causal_and_persistent_in_simulator():
 def test_asm_forward_prescaled_in_simulator(lens_q, lens_k, H, D, grid, dtype, causal, scale):
     """The PRESCALE form (Q~ = Q c rounded once per block, S^T seeded with -m c, softmax exp2(S))."""
     _run(lens_q, lens_k, H, D, dtype, scale=scale, causal=causal, grid=grid, prescale=True)
+
+
+def _run_text(txt, lens_q, lens_k, H, D, dtype, mode="lazy"):
+    """_run with a given kernel text (the product kernel cache bypassed)."""
+    saved = dict(_TXT)
+    hd = 128 if D > 64 else 64 if D > 32 else 32
+    _TXT.clear()
+    _TXT[(dtype, hd, 4, False, gen_fwd.product_prescale(dtype, hd, 4))] = txt
+    orig = asm_sim.Sim.__init__
+
+    def init(self, asm_text, dtype="bf16", soff_checked=True, **kw):
+        orig(self, asm_text, dtype, soff_checked, mode=mode)
+    asm_sim.Sim.__init__ = init
+    try:
+        _run(lens_q, lens_k, H, D, dtype)
+    finally:
+        asm_sim.Sim.__init__ = orig
+        _TXT.clear()
+        _TXT.update(saved)
+
+
+def test_simulator_catches_the_round3_d32_wait_bug():
+    """the D=32 tile's round-3 hardware bug -- a tile-end vmcnt sized for two DMA pieces
+    per tensor and tile when the D=32 tile issues one -- lets the next tile read ring slots whose DMA
+    has not landed. With lazy completion the simulator reads the stale slot and the result is wrong;
+    the correct count passes."""
+    gen_fwd.configure(32)
+    try:
+        g = gen_fwd.Gen("bf16")
+        good = gen_fwd.emit(g, gen_fwd.build(g)[0])
+        fixed = gen_fwd.pieces_wait
+        gen_fwd.pieces_wait = lambda: 4 * (gen_fwd.DIST - 1)     # the round-3 count
+        try:
+            g = gen_fwd.Gen("bf16")
+            bad = gen_fwd.emit(g, gen_fwd.build(g)[0])
+        finally:
+            gen_fwd.pieces_wait = fixed
+    finally:
+        gen_fwd.configure(64)
+    assert good != bad
+    _run_text(good, [70], [700], 1, 32, "bf16")
+    with pytest.raises(AssertionError):
+        _run_text(bad, [70], [700], 1, 32, "bf16")
+
+
+def test_simulator_catches_a_missing_wait_state():
+    """Removing the wait state between the VALU that writes the wave index and the v_readfirstlane
+    that reads it (round 3: three faulting dumps) raises HazardError in the simulator."""
+    txt = _kernel("bf16")
+    lines = txt.split("\n")
+    i = next(k for k, ln in enumerate(lines) if ln.strip().startswith("v_readfirstlane_b32"))
+    assert lines[i - 1].strip().startswith("s_nop"), lines[i - 2:i + 1]
+    bad = "\n".join(lines[:i - 1] + lines[i:])
+    with pytest.raises(asm_sim.HazardError):
+        _run_text(bad, [130], [200], 1, 64, "bf16")

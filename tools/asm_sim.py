@@ -11,10 +11,18 @@ fragment layouts of the MI355X guide (cdna_hip_programming.md §3):
                        4p..4p+3; lane i receives column i of rows 0..3
   v_permlane32_swap:   lanes 32..63 of vdst <-> lanes 0..31 of src
 
-Waves run round-robin between s_barriers; LDS-DMA lands at issue (the kernel's ring never
-reads a slot that a DMA of the same barrier interval writes, so this ordering is one the
-hardware may also produce). Buffer range checks include the SGPR offset (`soff_checked`).
-Wait counts and nops are no-ops here: the hazard pass of the generator is not simulated.
+Waves run round-robin between s_barriers. Buffer range checks include the SGPR offset (`soff_checked`).
+
+Completion of memory operations (mode `lazy`, the default): every vector-memory operation (loads,
+LDS-DMA, stores) and every LDS / SMEM operation is queued per wave in issue order and takes effect
+(registers or LDS written) only when an `s_waitcnt vmcnt(N)` / `lgkmcnt(N)` of that wave forces it
+(the latest point the hardware allows), or at s_endpgm: a consumer that the generator's counted
+waits do not cover reads the OLD contents and the result is wrong. Mode `eager` applies every
+operation at issue instead (an LDS-DMA that overwrites a ring slot other waves still read then
+shows up). Register hazards: `check_hazards` raises HazardError when an instruction reads a
+register closer to its writer than the gfx950 wait states allow (MFMA 32x32 result 12 states,
+16x16 8, VALU -> MFMA operand 2, transcendental -> VALU 1, VALU -> v_readfirstlane 1,
+VALU -> v_permlane 2); s_nop N counts N + 1 states, s_waitcnt none.
 
 Usage (tests/test_asm_sim.py): Sim(asm_text).run(grid, kernarg_bytes, memory).
 """
@@ -93,14 +101,33 @@ class Wave:
         self.m0 = 0
         self.pc = 0
         self.done = False
+        self.vmq = []        # pending vector-memory completions (callables), issue order
+        self.lgq = []        # pending LDS / SMEM completions
+        self.state = 0       # issued wait states (hazard checks)
+        self.wr = {}         # register -> (state after the writer, writer class, writer dst range)
+        self.pend = {}       # register -> pc of the queued load that will write it (lazy mode)
         self.v[0] = np.arange(64, dtype=np.uint32) + 64 * wave_id
         self.s[2], self.s[3], self.s[4] = wg
 
 
+class HazardError(RuntimeError):
+    pass
+
+
+# minimum distance in issued states from a writer class to a reader class (1 = back to back)
+_NEED = {('mfma32', None): 13, ('mfma16', None): 9, ('valu', 'mfma'): 3, ('trans', 'mfma'): 3,
+         ('trans', 'valu'): 2, ('trans', 'trans'): 2, ('trans', 'rfl'): 2, ('trans', 'perm'): 3,
+         ('valu', 'rfl'): 2, ('valu', 'perm'): 3}
+_TRANS = ('v_exp_f32', 'v_log_f32', 'v_rcp_f32')
+
+
 class Sim:
-    def __init__(self, asm_text, dtype='bf16', soff_checked=True):
+    def __init__(self, asm_text, dtype='bf16', soff_checked=True, mode='lazy', check_hazards=True):
         self.dtype = dtype
         self.soff_checked = soff_checked
+        assert mode in ('lazy', 'eager')
+        self.mode, self.check_hazards = mode, check_hazards
+        self.races = []      # lazy mode: (read pc, reading wave, DMA issue pc, issuing wave) of stale LDS reads
         lines = asm_text.split('\n')
         start = next(i for i, ln in enumerate(lines) if re.match(r'^fa_fwd_\w+:$', ln))
         end = next(i for i, ln in enumerate(lines) if ln.startswith('.Lfunc_end'))
@@ -232,7 +259,10 @@ class Sim:
     def run_wg(self, wg, karg, mem, max_steps):
         self.mem, self.karg = mem, karg
         self.lds = np.zeros(self.lds_bytes, dtype=np.uint8)
+        self.lds_pend = np.full(self.lds_bytes, -1, dtype=np.int64)   # lazy: issue pc * 16 + wave of a pending DMA
         waves = [Wave(self.nv, 256, i, wg) for i in range(self.nwaves)]
+        for i, w in enumerate(waves):
+            w.id = i
         for w in waves:
             w.s[0] = karg & 0xFFFFFFFF
             w.s[1] = karg >> 32
@@ -251,10 +281,98 @@ class Sim:
                     self.exec(w, op, args)
 
     # ---------------------------------------------------------------- semantics
+    # ---------------------------------------------------------------- completion queues / hazards
+    def _defer(self, w, q, fn, dst=None):
+        """Queue a completion; dst: destination register operand (lazy mode tracks it as pending)."""
+        if self.mode == 'eager':
+            fn()
+            return
+        regs = self._reg_list(dst) if dst else []
+        pc = w.pc - 1
+        for r in regs:
+            w.pend[r] = pc
+
+        def run(fn=fn, regs=regs, pc=pc):
+            fn()
+            for r in regs:
+                if w.pend.get(r) == pc:
+                    del w.pend[r]
+        q.append(run)
+
+    @staticmethod
+    def _drain(q, n):
+        while len(q) > n:
+            q.pop(0)()
+
+    def _reg_list(self, name):
+        m = _RANGE.match(name) or _ONE.match(name)
+        if not m or m.group(1) not in ('v', 'a'):
+            return []
+        f, lo = m.group(1), int(m.group(2))
+        hi = int(m.group(3)) if m.lastindex == 3 else lo
+        return [(f, i) for i in range(lo, hi + 1)]
+
+    def _hazard(self, w, op, a):
+        """Check the operand reads of `op` against their writers, then record its writes."""
+        if op.startswith('v_mfma'):
+            rk = 'mfma'
+            reads = [(x, 'ab') for x in a[1:3]] + ([(a[3], 'c')] if a[3] != '0' else [])
+            dst = a[0]
+        elif op in ('v_readfirstlane_b32', 'v_readlane_b32'):
+            rk, reads, dst = 'rfl', [(a[1], None)], None
+        elif op.startswith('v_permlane'):
+            rk, reads, dst = 'perm', [(a[0], None), (a[1], None)], a[0]
+        elif op.startswith('v_cmp'):
+            rk, reads, dst = 'valu', [(x, None) for x in a[1:]], None
+        elif op.startswith('v_'):
+            rk = 'trans' if op in _TRANS else 'valu'
+            reads, dst = [(x.lstrip('-'), None) for x in a[1:]], a[0]
+        else:
+            return
+        for name, role in reads:
+            for reg in self._reg_list(name):
+                if reg not in w.wr:
+                    continue
+                st, wk, wdst = w.wr[reg]
+                if wk.startswith('mfma'):
+                    if rk == 'mfma' and role == 'c' and wdst == a[0]:
+                        continue            # same-accumulator chain
+                    need = _NEED[(wk, None)]
+                else:
+                    need = _NEED.get((wk, rk), 1)
+                if w.state - st + 1 < need:
+                    raise HazardError(f'{op} {",".join(a)} reads {reg[0]}{reg[1]} {w.state - st + 1} states after '
+                                      f'its {wk} writer (needs {need}) at pc {w.pc - 1}')
+        if dst is not None:
+            wk = ('mfma32' if '32x32' in op else 'mfma16') if rk == 'mfma' else ('trans' if rk == 'trans' else 'valu')
+            for reg in self._reg_list(dst):
+                w.wr[reg] = (w.state + 1, wk, dst)
+
     def exec(self, w, op, a):
-        if op in ('s_nop', 's_waitcnt', 's_setprio'):
+        if op == 's_nop':
+            w.state += int(a[0], 0) + 1
+            return
+        if op == 's_waitcnt':
+            for part in a:
+                if part.startswith('vmcnt('):
+                    self._drain(w.vmq, int(part[6:-1]))
+                elif part.startswith('lgkmcnt('):
+                    self._drain(w.lgq, int(part[8:-1]))
+            return
+        if w.pend:
+            for x in a:
+                for r in self._reg_list(x.lstrip('-')):
+                    if r in w.pend:
+                        self.races.append((w.pc - 1, w.id, w.pend[r], w.id))
+                        break
+        if self.check_hazards:
+            self._hazard(w, op, a)
+        w.state += 1
+        if op == 's_setprio':
             return
         if op == 's_endpgm':
+            self._drain(w.vmq, 0)
+            self._drain(w.lgq, 0)
             w.done = True
             return
         if op == 's_branch':
@@ -273,8 +391,11 @@ class Sim:
             f, i, cnt = self.regs(w, a[0])
             _, b, _ = self.regs(w, a[1])
             addr = (int(w.s[b]) | (int(w.s[b + 1]) << 32)) + int(a[2], 0)
-            data = np.frombuffer(self.mem.read(addr, 4 * n).tobytes(), dtype=np.uint32)
-            w.s[i:i + n] = data
+            data = np.frombuffer(self.mem.read(addr, 4 * n).tobytes(), dtype=np.uint32).copy()
+
+            def done(w=w, i=i, n=n, data=data):
+                w.s[i:i + n] = data
+            self._defer(w, w.lgq, done)
             return
         if op.startswith('s_'):
             return self.salu(w, op, a)
@@ -291,6 +412,7 @@ class Sim:
             data = self.vread(w, a[1])
             for l in range(64):
                 self.mem.write(int(addr[l]) + off, np.frombuffer(data[l:l + 1].tobytes(), dtype=np.uint8))
+            self._defer(w, w.vmq, lambda: None)
             return
         return self.valu(w, op, a)
 
@@ -509,15 +631,29 @@ class Sim:
         if op == 'ds_bpermute_b32':
             addr = self.vread(w, a[1])
             src = self.vread(w, a[2])
-            self.vwrite(w, a[0], src[(addr // 4) % 64])
+            val = src[(addr // 4) % 64].copy()
+            self._defer(w, w.lgq, lambda w=w, d=a[0], val=val: self.vwrite(w, d, val), a[0])
             return
         addr = self.vread(w, a[1]).astype(np.int64) + off
         f, i, cnt = self.regs(w, a[0])
         dst = w.v if f == 'v' else w.a
+        if self.mode == 'lazy':
+            span = 16 if op == 'ds_read_b128' else 8
+            for l in range(64):
+                p = self.lds_pend[addr[l]:addr[l] + span]
+                if (p >= 0).any():
+                    q = int(p[p >= 0][0])
+                    self.races.append((w.pc - 1, w.id, q // 16, q % 16))
+                    break
         if op == 'ds_read_b128':
+            out = np.zeros((4, 64), dtype=np.uint32)
             for l in range(64):
                 b = self.lds[addr[l]:addr[l] + 16]
-                dst[i:i + 4, l] = np.frombuffer(b.tobytes(), dtype=np.uint32)
+                out[:, l] = np.frombuffer(b.tobytes(), dtype=np.uint32)
+
+            def done(dst=dst, i=i, out=out):
+                dst[i:i + 4] = out
+            self._defer(w, w.lgq, done, a[0])
             return
         if op == 'ds_read_b64_tr_b16':
             out = np.zeros((2, 64), dtype=np.uint32)
@@ -530,7 +666,10 @@ class Sim:
                         vals.append(int(b[0]) | (int(b[1]) << 8))
                     out[0, 16 * g + li] = vals[0] | (vals[1] << 16)
                     out[1, 16 * g + li] = vals[2] | (vals[3] << 16)
-            dst[i:i + 2] = out
+
+            def done(dst=dst, i=i, out=out):
+                dst[i:i + 2] = out
+            self._defer(w, w.lgq, done, a[0])
             return
         raise NotImplementedError(op)
 
@@ -555,17 +694,25 @@ class Sim:
         ok &= chk + n <= nrec
         addr = base + voff + off + soff
         if op == 'buffer_load_dwordx4':
+            data = [self.mem.read(int(addr[l]), 16).copy() if ok[l] else np.zeros(16, dtype=np.uint8)
+                    for l in range(64)]
             if lds:
-                for l in range(64):
-                    b = self.mem.read(int(addr[l]), 16) if ok[l] else np.zeros(16, dtype=np.uint8)
-                    la = w.m0 + 16 * l
-                    self.lds[la:la + 16] = b
+                m0 = w.m0
+                if self.mode == 'lazy':
+                    self.lds_pend[m0:m0 + 1024] = (w.pc - 1) * 16 + w.id
+
+                def done(m0=m0, data=data):
+                    for l in range(64):
+                        self.lds[m0 + 16 * l:m0 + 16 * l + 16] = data[l]
+                    self.lds_pend[m0:m0 + 1024] = -1
             else:
                 f, i, cnt = self.regs(w, dst)
                 tgt = w.v if f == 'v' else w.a
-                for l in range(64):
-                    b = self.mem.read(int(addr[l]), 16) if ok[l] else np.zeros(16, dtype=np.uint8)
-                    tgt[i:i + 4, l] = np.frombuffer(b.tobytes(), dtype=np.uint32)
+
+                def done(tgt=tgt, i=i, data=data):
+                    for l in range(64):
+                        tgt[i:i + 4, l] = np.frombuffer(data[l].tobytes(), dtype=np.uint32)
+            self._defer(w, w.vmq, done, None if lds else dst)
             return
         f, i, cnt = self.regs(w, src)
         srcr = w.v if f == 'v' else w.a
@@ -573,3 +720,4 @@ class Sim:
             if ok[l]:
                 words = srcr[i:i + n // 4, l].astype(np.uint32)
                 self.mem.write(int(addr[l]), np.frombuffer(words.tobytes(), dtype=np.uint8))
+        self._defer(w, w.vmq, lambda: None)     # stores count in vmcnt (applied at issue)

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round-4 product check: the whole -m gpu suite (all failures listed), smoke(), the default bench line.
+mkdir -p gpurun_out
+timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+    > gpurun_out/gputest_r04.txt 2>&1
+echo "suite rc=$?" >> gpurun_out/gputest_r04.txt
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r04.txt 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --no-extra > gpurun_out/bench_r04.json 2>&1
