@@ -889,6 +889,11 @@ def probe_filter(xs, keep_last=False):
         for x in body:
             if x.txt.startswith('v_exp_f32'):
                 x.txt, x.kind, x.cost = x.txt.replace('v_exp_f32', 'v_mov_b32'), 'valu', 4
+    if 'noor' in PROBE and tail and tail[0].txt.startswith('v_cmp_ne_u32 vcc, 0,'):
+        # timing probe: no OR-tree rescale test (a compare that never fires)
+        body = [x for x in body if not x.txt.startswith(('v_or3_b32', 'v_or_b32', 'v_and_b32'))]
+        r = tail[0].txt.split()[-1]
+        tail = [V(f'v_cmp_gt_u32 vcc, 0, {r}', 'vcc', [r])]
     return body + tail
 
 
@@ -1418,6 +1423,10 @@ def prologue_sections(g):
             p += g.dma('K', t + 1) + g.dma('V', t)
     # zero O, row sums, the V fragment buffer PV_B(-1) reads and P_B (PV_B(-1) of tile 0 adds
     # nothing); m = -inf
+    # PRESCALE: Q~ = Q c right after Q landed (the hazard pass counts the wait past the DMAs just
+    # issued), while the first K/V tiles are in flight
+    p.append(sec('qscale'))
+    p += q_prescale(g)
     p.append(sec('zero'))
     if QL_VGPR:
         p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(D)]
@@ -1439,7 +1448,7 @@ def prologue_sections(g):
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
     # (8 waves: phase 0 reads K2 as well: K0 K1 V0 K2 landed, all but the 3 youngest pieces)
     p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else pieces_wait()})')]
-    p += q_prescale(g) + [raw('s_barrier')]
+    p += [raw('s_barrier')]
     p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
     p += pstamp(PS_V + 4)
     # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
@@ -1454,29 +1463,33 @@ def prologue_sections(g):
     return p
 
 
-def q_prescale(g):
-    """PRESCALE: Q~ = rne16(Q c) in place (AGPR fragments of every block, after they landed):
-    per register the two 16-bit halves widened to fp32, multiplied by c, packed back. The
+def q_prescale(g, src=None):
+    """PRESCALE: Q~ = rne16(Q c) in place (AGPR fragments of every block, after they landed), or
+    from the VGPRs of `src` [(vgpr, agpr), ...] into the AGPRs (the persistent form's prefetched
+    next Q): per register the two 16-bit halves widened to fp32, multiplied by c, packed back. The
     per-register chains run 8 at a time, interleaved, so no op waits on its predecessor."""
     if not PRESCALE:
         return []
+    pairs = src or [(None, A_Q[X] + r) for X in BLOCKS for r in range(4 * NKS)]
     chains = []
-    k = 0
-    for X in BLOCKS:
-        for r in range(4 * NKS):
-            q = A_Q[X] + r
-            a, lo, hi = (V_S['A'] + (k % 8) * 4 + j for j in range(3))   # S registers: free before QK_A(0)
-            c = [Inst(f'v_accvgpr_read_b32 v{a}, a{q}', 'accr', rd=[f'a{q}'], wr=[f'v{a}'])]
+    for k, (vq, q) in enumerate(pairs):
+        if True:
+            a, lo, hi = (V_P['A'] + (k % 8) * 4 + j for j in range(3))   # P registers: free (P_B is zeroed later)
+            if vq is None:
+                c = [Inst(f'v_accvgpr_read_b32 v{a}, a{q}', 'accr', rd=[f'a{q}'], wr=[f'v{a}'])]
+            else:
+                c, a = [], vq
+                a_out = V_P['A'] + (k % 8) * 4 + 3
             if g.dtype == 'bf16':
                 c += [V(f'v_lshlrev_b32 v{lo}, 16, v{a}', lo, [a]), V(f'v_and_b32 v{hi}, 0xffff0000, v{a}', hi, [a])]
             else:
                 c += [V(f'v_cvt_f32_f16 v{lo}, v{a}', lo, [a]), V(f'v_lshrrev_b32 v{hi}, 16, v{a}', hi, [a]),
                       V(f'v_cvt_f32_f16 v{hi}, v{hi}', hi, [hi])]
+            o = a if vq is None else a_out
             c += [V(f'v_mul_f32 v{lo}, s{S_C}, v{lo}', lo, [lo]), V(f'v_mul_f32 v{hi}, s{S_C}, v{hi}', hi, [hi]),
-                  V(f'{g.cvt} v{a}, v{lo}, v{hi}', a, [lo, hi]),
-                  Inst(f'v_accvgpr_write_b32 a{q}, v{a}', 'accw', rd=[f'v{a}'], wr=[f'a{q}'])]
+                  V(f'{g.cvt} v{o}, v{lo}, v{hi}', o, [lo, hi]),
+                  Inst(f'v_accvgpr_write_b32 a{q}, v{o}', 'accw', rd=[f'v{o}'], wr=[f'a{q}'])]
             chains.append(c)
-            k += 1
     res = []
     for base in range(0, len(chains), 8):
         grp = chains[base:base + 8]
@@ -1589,6 +1602,9 @@ def prologue_persist(g):
     qcopy = [Inst(f'v_accvgpr_write_b32 a{A_Q[X] + r}, v{V_QN + 16 * xi + r}', 'accw',
                   rd=[f'v{V_QN + 16 * xi + r}'], wr=[f'a{A_Q[X] + r}'])
              for xi, X in enumerate(BLOCKS) for r in range(16)] + [raw('s_branch .Lqdone')]
+    if PRESCALE:    # the prefetched Q is scaled on its way into the AGPRs (no AGPR pass at .Lqdone)
+        qcopy = q_prescale(g, src=[(V_QN + 16 * xi + r, A_Q[X] + r) for xi, X in enumerate(BLOCKS)
+                                   for r in range(16)]) + [raw('s_branch .Lqdone')]
     if not PERSIST_Q:
         qcopy = []
     qload = [label('.Lqload')] + sc['qload']
@@ -1623,7 +1639,9 @@ def prologue_persist(g):
         st[i] = raw(f's_waitcnt vmcnt({n})')
         return st
     # the first wait waits for Q, K0, K1, V0: younger are K2 V1 K3 V2 (8 pieces) and the next Q's loads
-    pb2 = [label('.Lqdone'), S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + sc['dma'] + pf + \
+    qs = ([S('s_cmp_lg_u32 s101, 0'), raw('s_cbranch_scc1 .Lqsdone')] + sc['qscale'] + [label('.Lqsdone')]
+          if PRESCALE else [])
+    pb2 = [label('.Lqdone'), S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + sc['dma'] + qs + pf + \
         sc['zero'] + start_with_wait(pieces_wait() + nq)
     # K0..K3 / V0..V2 came from the previous block's tail: the descriptor sets only walk as the
     # prologue's DMAs would have; younger than K0 K1 V0 are the tail's last 8 pieces, this

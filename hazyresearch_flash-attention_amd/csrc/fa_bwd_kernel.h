@@ -381,7 +381,13 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                     // full tile (wave-uniform test): the four atomics without per-lane guards
                     float *base = dqa + (int64_t)(qd + 16 * qh + 4 * g4) * dqa_row + d;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) atomicAdd(base + i * dqa_row, acc[i]);
+                    for (int i = 0; i < 4; ++i) {
+#ifdef FA_BWD_PROBE_NOATOMIC   // timing probe only (tools/ab_libs.sh builds): no dQ atomics, wrong dQ
+                        if (acc[i] == 1.2345e-30f) base[i * dqa_row] = acc[i];
+#else
+                        atomicAdd(base + i * dqa_row, acc[i]);
+#endif
+                    }
                 } else if (d < head_dim) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {

@@ -137,3 +137,65 @@ def test_c5_exact_grid_kvpacked_cross_fwd_bwd():
     _check_fwd_bwd(lambda a, b: fi.flash_attn_unpadded_kvpacked_func(a, b, cu_q, cu_k, Sq, Sk, 0.0),
                    (q, kv), lambda gr: (gr[0], gr[1][:, 0], gr[1][:, 1]), q, k, v, B, Sq, Sk, H, D, causal=False)
     _check_lse(q.detach(), k, v, cu_q, cu_k, B, Sq, Sk, H, D, causal=False)
+
+
+def _check_fwd_bwd_chunked(out, g, grads, q, k, v, B, Sq, Sk, H, D, causal, chunk):
+    """The 2x rule over the whole grid with the oracle run in batch chunks (attention is per sequence,
+    so every chunk's fp32 and low-precision autograd is exact for its rows): the maximum error over
+    all chunks against twice the maximum baseline error over all chunks, for out, dq, dk, dv."""
+    worst = {n: [0.0, 0.0] for n in ("out", "dq", "dk", "dv")}
+    for b0 in range(0, B, chunk):
+        b1 = min(B, b0 + chunk)
+        n = b1 - b0
+        q4 = q[b0 * Sq:b1 * Sq].detach().view(n, Sq, H, D).requires_grad_()
+        k4 = k[b0 * Sk:b1 * Sk].detach().view(n, Sk, H, D).requires_grad_()
+        v4 = v[b0 * Sk:b1 * Sk].detach().view(n, Sk, H, D).requires_grad_()
+        g4 = g[b0 * Sq:b1 * Sq].view(n, Sq, H, D)
+        for upcast in (True, False):
+            o, _ = attention_ref(q4, k4, v4, causal=causal, upcast=upcast, reorder_ops=not upcast)
+            gr = torch.autograd.grad(o, (q4, k4, v4), g4)
+            if upcast:
+                ref, rgr = o.detach(), gr
+            else:
+                pt, pgr = o.detach(), gr
+        mine = (out[b0 * Sq:b1 * Sq].view(n, Sq, H, D),) + tuple(
+            t[r0:r1].view(n, S, H, D) for t, (r0, r1, S) in
+            zip(grads, ((b0 * Sq, b1 * Sq, Sq), (b0 * Sk, b1 * Sk, Sk), (b0 * Sk, b1 * Sk, Sk))))
+        for name, a, rr, pp in zip(("out", "dq", "dk", "dv"), mine, (ref,) + tuple(rgr), (pt,) + tuple(pgr)):
+            worst[name][0] = max(worst[name][0], (a.float() - rr.float()).abs().max().item())
+            worst[name][1] = max(worst[name][1], max_err_bound(pp, rr))
+        del ref, pt, rgr, pgr, q4, k4, v4
+    for name, (e, bnd) in worst.items():
+        assert e <= bnd, f"{name}: max err {e} > {bnd} (2x rule over the whole grid)"
+
+
+def test_c4_exact_grid_d128_causal_backward():
+    """C4 (B16 H12 S4096 D128 causal) forward + backward at the exact grid, the
+    gradients under the 2x rule against autograd of the oracle run in 2-batch chunks."""
+    B, S, H, D = 16, 4096, 12, 128
+    q, k, v, cu, _ = _inputs(B, S, S, H, D, torch.bfloat16, seed=42)
+    q, k, v = (t.requires_grad_() for t in (q, k, v))
+    out = _fi().flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0, causal=True)
+    g = torch.randn(out.shape, generator=torch.Generator(device=DEV).manual_seed(43), device=DEV).to(out.dtype)
+    grads = torch.autograd.grad(out, (q, k, v), g)
+    _check_fwd_bwd_chunked(out.detach(), g, grads, q, k, v, B, S, S, H, D, causal=True, chunk=2)
+
+
+def test_north_star_grid_all_heads_persistent_forward():
+    """the bench workload (B8 H12 S2048 D64 bf16, 768 blocks, the persistent asm form
+    FA_IMPL_AUTO picks) against the fp32 oracle on all 96 heads under the 2x rule, with the LSE."""
+    from flash_attn import flash_attn_hip as hip
+    B, S, H, D = 8, 2048, 12, 64
+    assert hip.fwd_kernel_name(B, H, D, S, S, torch.bfloat16) == "fa_fwd_d64p_bf16_asm"
+    q, k, v, cu, _ = _inputs(B, S, S, H, D, torch.bfloat16, seed=61)
+    out = _fi().flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
+    worst = [0.0, 0.0]
+    with torch.no_grad():
+        for b0 in range(0, B, 2):
+            q4, k4, v4 = (t[b0 * S:(b0 + 2) * S].view(2, S, H, D) for t in (q, k, v))
+            ref, _ = attention_ref(q4, k4, v4)
+            pt, _ = attention_ref(q4, k4, v4, upcast=False, reorder_ops=True)
+            worst[0] = max(worst[0], (out[b0 * S:(b0 + 2) * S].view(2, S, H, D).float() - ref.float()).abs().max().item())
+            worst[1] = max(worst[1], max_err_bound(pt, ref))
+    assert worst[0] <= worst[1], f"max err {worst[0]} > {worst[1]}"
+    _check_lse(q, k, v, cu, cu, B, S, S, H, D, causal=False, chunk=2)

@@ -21,8 +21,14 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 
 
 def build(out_dir, extra):
-    s = os.path.join(out_dir, "pstamps.s")
-    subprocess.check_call([sys.executable, GEN, "--out", s, "--persist", "1", "--probe", "pstamps"] + extra.split())
+    s = os.path.join(out_dir, "pstamps_" + "".join(c if c.isalnum() else "_" for c in extra) + ".s")
+    extra = extra.split()
+    probes = ["pstamps"]
+    if "--probe" in extra:     # merge the variant's own probe switches with the stamps
+        i = extra.index("--probe")
+        probes.append(extra[i + 1])
+        del extra[i:i + 2]
+    subprocess.check_call([sys.executable, GEN, "--out", s, "--persist", "1", "--probe", ",".join(probes)] + extra)
     subprocess.check_call([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
                            s, "-o", s[:-2] + ".o"])
     subprocess.check_call([f"{LLVM}/ld.lld", "-shared", s[:-2] + ".o", "-o", s[:-2] + ".hsaco"])
