@@ -27,7 +27,7 @@ _TXT = {}
 def _kernel(dtype, hd=64, waves=4, persist=False, prescale=None):
     """prescale: None = the product setting of build.py for this form (gen_fwd.product_prescale)."""
     if prescale is None:
-        prescale = gen_fwd.product_prescale(dtype, hd, waves)
+        prescale = gen_fwd.product_prescale(dtype, hd, waves, persist)
     key = (dtype, hd, waves, persist, prescale)
     if key not in _TXT:
         gen_fwd.configure(hd, waves)
@@ -79,7 +79,7 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4,
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
     hd = 128 if D > 64 else 64 if D > 32 else 32
     if prescale is None:
-        prescale = gen_fwd.product_prescale(dtype, hd, waves)
+        prescale = gen_fwd.product_prescale(dtype, hd, waves, bool(grid))
     asm_sim.Sim(_kernel(dtype, hd, waves, bool(grid), prescale), dtype).run(
         (grid, 1, 1) if grid else (nqb, H, B), pa, mem)
     o = asm_sim.from16(mem.get(po).view(np.uint16).astype(np.uint32), dtype).reshape(tq, H, D)
@@ -264,7 +264,7 @@ def _run_text(txt, lens_q, lens_k, H, D, dtype, mode="lazy"):
     saved = dict(_TXT)
     hd = 128 if D > 64 else 64 if D > 32 else 32
     _TXT.clear()
-    _TXT[(dtype, hd, 4, False, gen_fwd.product_prescale(dtype, hd, 4))] = txt
+    _TXT[(dtype, hd, 4, False, gen_fwd.product_prescale(dtype, hd, 4, False))] = txt
     orig = asm_sim.Sim.__init__
 
     def init(self, asm_text, dtype="bf16", soff_checked=True, **kw):
