@@ -71,6 +71,9 @@ V_SEED = {'A': 212, 'B': 228}   # PRESCALE: -m c broadcast over the 16 registers
 KFIRST = True          # phase 1: K(t+1) fragment reads ahead of the V^T reads (D = 64)
 KFIRST_LO = 2          # softmax-stream position of the first K read with KFIRST
 LGKM_XPHASE = True     # counted lgkmcnt waits may count LDS reads of the previous phase
+MFMA_ZERO = True       # prologue: O, row sums, V buffer zeroed by MFMAs of a zero operand (D <= 64)
+ORDET_ANDOR = True     # ORDET: the last P word enters the test by one v_and_or_b32 (mask in V_MTHR)
+PHASE_TAIL = 1         # ORDET test issued before the phase's last PHASE_TAIL MFMAs, its branch after them
 
 
 def set_geometry(r, dist):
@@ -475,13 +478,21 @@ class Gen:
             steps.append((cvt_at[q], 2, V(f'{self.cvt} v{P + q}, v{a}, v{b}', P + q, [a, b])))
         if ortest:
             T = V_TMP[X] if V_ORT is None else V_ORT
-            groups = [(0, 1, 2)] + [(2 * k + 1, 2 * k + 2) for k in range(1, 7)] + [(15,)]
+            last = 14 if ORDET_ANDOR else 15
+            groups = [(0, 1, 2)] + [(2 * k + 1, 2 * k + 2) for k in range(1, 7)] + ([] if ORDET_ANDOR else [(15,)])
             for gi, grp in enumerate(groups):
                 srcs = ([] if gi == 0 else [T]) + [P + q for q in grp]
                 op = 'v_or3_b32' if len(srcs) == 3 else 'v_or_b32'
                 steps.append((cvt_at[max(grp)] + 3, 3, V(f'{op} v{T}, ' + ', '.join(f'v{r}' for r in srcs), T, srcs)))
-            end = cvt_at[15] + 3
+            end = cvt_at[last] + 3
             steps.append((end + 1, 3, V(f'v_and_b32 v{T}, 0x40004000, v{T}', T, [T])))
+            if ORDET_ANDOR:
+                # the last P word joins after the mask: (P15 & M) | T, M = 0x40004000 in V_MTHR
+                # (unused by the OR test): one dependent step between the last cvt and the compare
+                end = cvt_at[15] + 3
+                M = V_MTHR[X]
+                steps.append((end, 3, Inst(f'v_and_or_b32 v{T}, v{P + 15}, v{M}, v{T}', 'valu', 4,
+                                           rd=[f'v{P + 15}', f'v{M}', f'v{T}'], wr=[f'v{T}'])))
             steps.append((end + 2, 3, V(f'v_cmp_ne_u32 vcc, 0, v{T}', 'vcc', [T])))
         return [x for _, _, x in sorted(steps, key=lambda z: (z[0], z[1]))]
 
@@ -784,12 +795,22 @@ class Gen:
         return e
 
     # ------------------------------------------------------------------ phases
+    @staticmethod
+    def tail_test(sm, mf):
+        """PHASE_TAIL: the rescale test (and everything before it in the fill) is issued before
+        the phase's last PHASE_TAIL MFMAs and the branch after them, so the compare's latency
+        runs under those MFMAs instead of stalling the branch."""
+        if PHASE_TAIL and len(sm) >= 2 and sm[-1].kind == 'br' and len(mf) > PHASE_TAIL:
+            sm[-2].deadline = len(mf) - PHASE_TAIL
+            sm[-1].not_before = len(mf)
+
     def phase1(self, t, masked=False, last=False, rescue=None, kv_next=False):
         """Tile t, phase 1: QK_B(t) + PV_B(t-1) + row sums beside block A's softmax of tile t,
         K(t+1) fragment reads and the K(t+1+DIST) DMA."""
         qkb = self.qk('B', t)
         mf = qkb + self.pv_sum('B', t - 1)[0]
         sm = self.softmax('A', masked, rescue)
+        self.tail_test(sm, mf)
         side = [] if last else self.kreads(t + 1)
         k_lo = 16
         if NBK == 1:
@@ -819,6 +840,7 @@ class Gen:
         pv, use = self.pv_sum('A', t)
         mf = qk + pv
         sm = self.softmax('B', masked, rescue)
+        self.tail_test(sm, mf)
         vr = []
         for f, ins in ([] if VREADS_P1 else self.vreads(t)):
             ins.deadline = max(0, len(qk) + use[f] - 3)
@@ -894,6 +916,9 @@ def probe_filter(xs, keep_last=False):
         body = [x for x in body if not x.txt.startswith(('v_or3_b32', 'v_or_b32', 'v_and_b32'))]
         r = tail[0].txt.split()[-1]
         tail = [V(f'v_cmp_gt_u32 vcc, 0, {r}', 'vcc', [r])]
+    if 'nobrdep' in PROBE and tail and tail[0].txt.startswith('v_cmp_ne_u32 vcc, 0,'):
+        # timing probe: the OR tree stays, the branch tests a register it does not produce
+        tail = [V(f'v_cmp_gt_u32 vcc, 0, v{V_ONEF}', 'vcc', [V_ONEF])]
     return body + tail
 
 
@@ -1296,7 +1321,7 @@ def prologue_sections(g):
           S('s_mul_i32 s93, s92, s67'), S('s_mul_hi_u32 s94, s92, s67'),
           S(f's_add_u32 s{S_LD}, s48, s93'), S(f's_addc_u32 s{S_LD + 1}, s49, s94'),
           S(f's_lshl_b32 s{S_LD + 2}, s77, 2'), S(f's_mov_b32 s{S_LD + 3}, 0x00020000')]
-    p += [S(f's_mov_b32 s{S_C}, s68'), S(f's_mov_b32 s{S_THR}, s69'),
+    p += [S(f's_mov_b32 s{S_C}, s68'), S(f's_mov_b32 s{S_THR}, s{68 if PRESCALE else 69}'),
           S(f's_add_u32 s{S_NT}, s79, 63'), S(f's_lshr_b32 s{S_NT}, s{S_NT}, 6'),
           # causal: the q-block's rows end at 256 (qb + 1), so 4 (qb + 1) tiles at most, and the
           # diagonal band (masked loop) starts at tile 4 qb
@@ -1431,13 +1456,36 @@ def prologue_sections(g):
     if QL_VGPR:
         p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(D)]
         p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(A_L['A'], A_L['B'] + 4)]
-    else:
-        p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(A_ONES)]
     vf1 = A_VF + KFB * ((-1) % NBV)
-    p += [Inst(f'v_accvgpr_write_b32 a{vf1 + r}, v32', 'accw', rd=['v32'], wr=[f'a{vf1 + r}'])
-          for r in range(KFB)]
-    p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
-    p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in (V_MTHR['A'], V_MTHR['B'], V_MC['A'], V_MC['B'])]
+    if QL_VGPR or not MFMA_ZERO:
+        if not QL_VGPR:
+            p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(A_ONES)]
+        p += [Inst(f'v_accvgpr_write_b32 a{vf1 + r}, v32', 'accw', rd=['v32'], wr=[f'a{vf1 + r}'])
+              for r in range(KFB)]
+        p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
+    else:
+        # P_B = 0 first; then O, the row sums and the V fragment buffer PV_B(-1) reads are MFMA
+        # products of that zero with C = 0 (16 / 4 AGPRs per instruction instead of one)
+        p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
+        z = V_P['B']
+        for lo, n in ((0, A_ONES), (vf1, KFB)):
+            r = lo
+            while r < lo + n:
+                if lo + n - r >= 16 and r % 16 == 0:
+                    p.append(Inst(f'{g.mf32} {as_(r, 16)}, {vs(z, 4)}, {vs(z, 4)}, 0', 'mfma', 8,
+                                  rd=rv(z, 4), wr=ra(r, 16), pipe=32))
+                    r += 16
+                elif lo + n - r >= 4 and r % 4 == 0:
+                    p.append(Inst(f'{g.mf16} {as_(r, 4)}, {vs(z, 4)}, {vs(z, 4)}, 0', 'mfma', 8,
+                                  rd=rv(z, 4), wr=ra(r, 4), pipe=16))
+                    r += 4
+                else:
+                    p.append(Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']))
+                    r += 1
+    p += [V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF]) for r in (V_MC['A'], V_MC['B'])]
+    # V_MTHR: the max test's threshold, or with ORDET the OR test's mask (ORDET_ANDOR)
+    p += [V(f'v_mov_b32 v{r}, 0x40004000', r, []) if ORDET else V(f'v_mov_b32 v{r}, v{V_NEGINF}', r, [V_NEGINF])
+          for r in sorted({V_MTHR['A'], V_MTHR['B']})]
     if PRESCALE:
         p += [V(f'v_mov_b32 v{r}, {-SEED0!r}', r, []) for r in (V_MC['A'], V_MC['B'])]
         p += [V(f'v_mov_b32 v{r}, {SEED0!r}', r, []) for X in BLOCKS for r in range(V_SEED[X], V_SEED[X] + 16)]
@@ -1470,11 +1518,14 @@ def q_prescale(g, src=None):
     per-register chains run 8 at a time, interleaved, so no op waits on its predecessor."""
     if not PRESCALE:
         return []
+    if 'noqs' in PROBE:     # timing probe: Q copied unscaled (the pre-scale's price)
+        return [Inst(f'v_accvgpr_write_b32 a{q}, v{vq}', 'accw', rd=[f'v{vq}'], wr=[f'a{q}']) for vq, q in (src or [])]
     pairs = src or [(None, A_Q[X] + r) for X in BLOCKS for r in range(4 * NKS)]
     chains = []
     for k, (vq, q) in enumerate(pairs):
         if True:
-            a, lo, hi = (V_P['A'] + (k % 8) * 4 + j for j in range(3))   # P registers: free (P_B is zeroed later)
+            # P registers: free (P_B is zeroed later); lo:hi an even-aligned pair (v_pk_mul_f32)
+            lo, hi, a = (V_P['A'] + (k % 8) * 4 + j for j in range(3))
             if vq is None:
                 c = [Inst(f'v_accvgpr_read_b32 v{a}, a{q}', 'accr', rd=[f'a{q}'], wr=[f'v{a}'])]
             else:
@@ -1486,7 +1537,9 @@ def q_prescale(g, src=None):
                 c += [V(f'v_cvt_f32_f16 v{lo}, v{a}', lo, [a]), V(f'v_lshrrev_b32 v{hi}, 16, v{a}', hi, [a]),
                       V(f'v_cvt_f32_f16 v{hi}, v{hi}', hi, [hi])]
             o = a if vq is None else a_out
-            c += [V(f'v_mul_f32 v{lo}, s{S_C}, v{lo}', lo, [lo]), V(f'v_mul_f32 v{hi}, s{S_C}, v{hi}', hi, [hi]),
+            # (s[S_C:S_C+1] = (c, c) with PRESCALE: S_THR holds c, the max test that reads it is off)
+            c += [Inst(f'v_pk_mul_f32 v[{lo}:{hi}], v[{lo}:{hi}], s[{S_C}:{S_C + 1}]', 'valu', 4,
+                       rd=[f'v{lo}', f'v{hi}', f's{S_C}', f's{S_C + 1}'], wr=[f'v{lo}', f'v{hi}']),
                   V(f'{g.cvt} v{o}, v{lo}, v{hi}', o, [lo, hi]),
                   Inst(f'v_accvgpr_write_b32 a{q}, v{o}', 'accw', rd=[f'v{o}'], wr=[f'a{q}'])]
             chains.append(c)
@@ -1598,15 +1651,16 @@ def prologue_persist(g):
     nxt += make_desc(S_NQD, 40, 76, 62, 54, 55, 77)
     lanes_t = [V(f'v_and_b32 v16, 31, v{V_TID}', 16, [V_TID]), V(f'v_bfe_u32 v17, v{V_TID}, 5, 1', 17, [V_TID]),
                V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
-    pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + nxt + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + \
+    dec2 = [] if 'nodec2' in PROBE else [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
+    pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + nxt + dec2 + \
         sc['state'] + lanes_t + \
-        sc['rows'] + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
+        sc['rows'] + pstamp(PS_V + 4, 'pstA') + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
     qcopy = [Inst(f'v_accvgpr_write_b32 a{A_Q[X] + r}, v{V_QN + 16 * xi + r}', 'accw',
                   rd=[f'v{V_QN + 16 * xi + r}'], wr=[f'a{A_Q[X] + r}'])
              for xi, X in enumerate(BLOCKS) for r in range(16)] + [raw('s_branch .Lqdone')]
     if PRESCALE:    # the prefetched Q is scaled on its way into the AGPRs (no AGPR pass at .Lqdone)
         qcopy = q_prescale(g, src=[(V_QN + 16 * xi + r, A_Q[X] + r) for xi, X in enumerate(BLOCKS)
-                                   for r in range(16)]) + [raw('s_branch .Lqdone')]
+                                   for r in range(16)]) + pstamp(PS_V + 4, 'pstB') + [raw('s_branch .Lqdone')]
     if not PERSIST_Q:
         qcopy = []
     qload = [label('.Lqload')] + sc['qload']
@@ -1614,11 +1668,12 @@ def prologue_persist(g):
     pf = [S(f's_lshl_b32 s93, s{S_WAVE}, 6'), S(f's_lshl_b32 s90, s{S_NQB}, 8'), S('s_add_u32 s93, s93, s90')]
     for xi, (X, xo) in enumerate((('A', 0), ('B', 32)) if PERSIST_Q else ()):
         pf += [V('v_add_u32 v39, s93, v16', 39, [16])] + ([V(f'v_add_u32 v39, {xo}, v39', 39, [39])] if xo else [])
+        pf += [V('v_mul_lo_u32 v38, v39, s62', 38, [39])]     # row base: one multiply per block
         for ks in range(NKS):
             o = V_QNOFF + 4 * xi + ks
             pf += [V(f'v_add_u32 v40, {2 * ks}, v17', 40, [17]), V('v_lshlrev_b32 v41, 3, v40', 41, [40]),
                    V('v_cmp_gt_u32 vcc, s74, v41', 'vcc', [41]),
-                   V('v_mul_lo_u32 v42, v39, s62', 42, [39]), V('v_lshl_add_u32 v42, v40, 4, v42', 42, [40, 42]),
+                   V('v_lshl_add_u32 v42, v40, 4, v38', 42, [40, 38]),
                    Inst(f'v_cndmask_b32 v{o}, v31, v42, vcc', 'valu', rd=['v31', 'v42', 'vcc'], wr=[f'v{o}'])]
     for xi, X in enumerate(BLOCKS if PERSIST_Q else ''):
         for ks in range(NKS):
@@ -1761,10 +1816,17 @@ def stamp_exit():
 PS_V = 244
 
 
-def pstamp(lo):
+def pstamp(lo, at=None):
+    """at: 'pstA' (after the block's decode and row offsets) / 'pstB' (after the Q copy): the
+    loop-start stamp moved there by the probe of that name (prologue split)."""
     if 'pstamps' not in PROBE:
         return []
-    return [raw('s_memtime s[96:97]'), raw('s_waitcnt lgkmcnt(0)'), raw(f'v_mov_b32 v{lo}, s96'),
+    if lo == PS_V + 4 and (at or 'start') not in PROBE and ('pstA' in PROBE or 'pstB' in PROBE):
+        return []
+    if at is not None and at not in PROBE:
+        return []
+    clk = 's_memrealtime' if 'pstrt' in PROBE else 's_memtime'    # pstrt: the global 100 MHz clock
+    return [raw(f'{clk} s[96:97]'), raw('s_waitcnt lgkmcnt(0)'), raw(f'v_mov_b32 v{lo}, s96'),
             raw(f'v_mov_b32 v{lo + 1}, s97')]
 
 
@@ -2043,6 +2105,9 @@ def main():
     ap.add_argument('--kfirst', type=int, default=None, help='K(t+1) reads first in phase 1 (value: first position)')
     ap.add_argument('--prescale', type=int, default=None, help='Q pre-scaled by c, S^T seeded with -m c (D = 64, 4 waves)')
     ap.add_argument('--xphase', type=int, default=None, help='counted lgkmcnt waits across phase marks')
+    ap.add_argument('--mzero', type=int, default=None, help='prologue zeroing by MFMAs (D <= 64)')
+    ap.add_argument('--andor', type=int, default=None, help='ORDET: last P word joins the test by v_and_or_b32')
+    ap.add_argument('--ptail', type=int, default=None, help='rescale test before the last N MFMAs of its phase')
     args = ap.parse_args()
     global DUMP
     if args.dump:
@@ -2069,7 +2134,14 @@ def main():
         EXP_LAG, CVT_LAG = (int(x) for x in args.lag.split(','))
     if args.mcbanks is not None:
         MC_BANKS = bool(args.mcbanks)
-    global KFIRST, KFIRST_LO, LGKM_XPHASE, PRESCALE
+    global KFIRST, KFIRST_LO, LGKM_XPHASE, PRESCALE, PHASE_TAIL
+    if args.ptail is not None:
+        PHASE_TAIL = args.ptail
+    global ORDET_ANDOR, MFMA_ZERO
+    if args.mzero is not None:
+        MFMA_ZERO = bool(args.mzero)
+    if args.andor is not None:
+        ORDET_ANDOR = bool(args.andor)
     prescale = product_prescale(args.dtype, args.hd, args.waves, bool(args.persist)) if args.prescale is None else bool(args.prescale)
     if args.kfirst is not None:
         KFIRST, KFIRST_LO = args.kfirst > 0, max(0, args.kfirst)

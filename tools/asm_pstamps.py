@@ -100,6 +100,14 @@ def main():
             prev = slice((rnd - 1) * grid, rnd * grid)
             d["seam_gap"] = np.median(tb[sel] - ts[prev])
         res[f"round{rnd}"] = {k: round(float(v), 1) for k, v in d.items()}
+    # finish spread (--gen "--probe pstrt": stamps on the global 100 MHz clock, so comparable across
+    # CUs): per workgroup the seam stamp of its last block (median over waves), us after the first entry
+    if rounds and "pstrt" in args.gen:
+        last = slice((rounds - 1) * grid, rounds * grid)
+        fin = (np.median(ts[last], axis=1) - tb.min()) / 100.0
+        res["finish_us"] = {"min": round(float(fin.min()), 2), "med": round(float(np.median(fin)), 2),
+                            "p90": round(float(np.percentile(fin, 90)), 2), "max": round(float(fin.max()), 2),
+                            "by_wg_mod8_med": [round(float(np.median(fin[x::8])), 2) for x in range(8)]}
     print(json.dumps(res), flush=True)
 
 

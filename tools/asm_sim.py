@@ -492,6 +492,15 @@ class Sim:
                 res = {'gt': p > q, 'eq': p == q, 'lt': p < q, 'ne': p != q}[kind[:-4]]
             w.vcc = np.asarray(res, dtype=bool)
             return
+        if op == 'v_pk_mul_f32':      # 64-bit operands: two fp32 lanes, default op_sel
+            halves = lambda tok: (lambda f, lo, n: [f'{f}{lo}', f'{f}{lo + 1}'])(*self.regs(w, tok))
+            (d0, d1), (x0, x1), (y0, y1) = halves(a[0]), halves(a[1]), halves(a[2])
+            with np.errstate(all='ignore'):
+                r0 = (self.fread(w, x0) * self.fread(w, y0)).astype(np.float32)
+                r1 = (self.fread(w, x1) * self.fread(w, y1)).astype(np.float32)
+            self.vwrite(w, d0, r0.view(U))
+            self.vwrite(w, d1, r1.view(U))
+            return
         if op == 'v_cndmask_b32':
             s0, s1 = self.vread(w, a[1]), self.vread(w, a[2])
             self.vwrite(w, a[0], np.where(w.vcc, s1, s0).astype(U))
@@ -531,6 +540,8 @@ class Sim:
                 r = src[0] | src[1]
             elif op == 'v_or3_b32':
                 r = src[0] | src[1] | src[2]
+            elif op == 'v_and_or_b32':
+                r = (src[0] & src[1]) | src[2]
             elif op == 'v_xor_b32':
                 r = src[0] ^ src[1]
             elif op == 'v_bfe_u32':
