@@ -71,6 +71,8 @@ V_SEED = {'A': 212, 'B': 228}   # PRESCALE: -m c broadcast over the 16 registers
 KFIRST = True          # phase 1: K(t+1) fragment reads ahead of the V^T reads (D = 64)
 KFIRST_LO = 2          # softmax-stream position of the first K read with KFIRST
 LGKM_XPHASE = True     # counted lgkmcnt waits may count LDS reads of the previous phase
+FIRST_MAX = True       # prologue: tile 0's row max sets the starting shift (no rescale at tile 0)
+LAST_UNMASKED = True   # last tile: unmasked copy when every row sees the whole tile
 MFMA_ZERO = True       # prologue: O, row sums, V buffer zeroed by MFMAs of a zero operand (D <= 64)
 ORDET_ANDOR = True     # ORDET: the last P word enters the test by one v_and_or_b32 (mask in V_MTHR)
 PHASE_TAIL = 1         # ORDET test issued before the phase's last PHASE_TAIL MFMAs, its branch after them
@@ -717,6 +719,36 @@ class Gen:
         b.append(raw('s_nop 2'))
         b.append(raw(f's_branch {ret}'))
         return b
+
+    def first_max(self):
+        """FIRST_MAX (prologue, after QK_A(0)): QK_B(0) into S_B as well, then per block the
+        row max of tile 0 sets the starting shift (m c = max c + delta, as the rescale block
+        would, O and the row sums being zero): tile 0 then passes the ORDET test instead of always
+        taking the out-of-line rescale. PRESCALE: the seeds and S_A(0) (already seeded) move by
+        the shift, S_B(0) is recomputed by tile 0's QK_B with the new seed. Only when tile 0 is
+        unmasked for every row (S_MSTART > 0): a masked first tile keeps the initial state (the
+        max over keys a row may not see could shift its P out of range)."""
+        out = self.qk('B', 0)
+        out.append(Inst(f's_cmp_lg_u32 s{S_MSTART}, 0', 'salu', 2, rd=[f's{S_MSTART}']))
+        out.append(Inst('s_cselect_b64 s[96:97], -1, 0', 'salu', 2, wr=['s96', 's97']))
+        for X in BLOCKS:
+            T, mc = V_TMP[X], V_MC[X]
+            out += self.max_ops(X)[:-1]            # v{T+6}: tile max of S_X
+            if PRESCALE:
+                # S holds s~ - m c: T6 + delta is the shift (> 0: m c starts at -SEED0)
+                out.append(V(f'v_add_f32 v{T + 7}, {ORDET_DELTA[self.dtype]!r}, v{T + 6}', T + 7, [T + 6]))
+                out.append(Inst(f'v_cndmask_b32 v{T + 7}, 0, v{T + 7}, s[96:97]', 'valu', 4,
+                                rd=[f'v{T + 7}', 's96', 's97'], wr=[f'v{T + 7}']))
+                out.append(V(f'v_add_f32 v{mc}, v{mc}, v{T + 7}', mc, [mc, T + 7]))
+                out += [V(f'v_sub_f32 v{r}, v{r}, v{T + 7}', r, [r, T + 7]) for r in range(V_SEED[X], V_SEED[X] + 16)]
+                if X == 'A':
+                    out += [V(f'v_sub_f32 v{r}, v{r}, v{T + 7}', r, [r, T + 7]) for r in range(V_S['A'], V_S['A'] + 32)]
+            else:
+                out.append(V(f'v_mul_f32 v{T + 7}, s{S_C}, v{T + 6}', T + 7, [T + 6]))
+                out.append(V(f'v_add_f32 v{T + 7}, {ORDET_DELTA[self.dtype]!r}, v{T + 7}', T + 7, [T + 7]))
+                out.append(Inst(f'v_cndmask_b32 v{mc}, v{mc}, v{T + 7}, s[96:97]', 'valu', 4,
+                                rd=[f'v{mc}', f'v{T + 7}', 's96', 's97'], wr=[f'v{mc}']))
+        return out
 
     def scale_acc(self, X):
         """Rescale tail: m*c copies (MC_BANKS), O_X and the row sums times alpha (v{T})."""
@@ -1501,6 +1533,8 @@ def prologue_sections(g):
     p += pstamp(PS_V + 4)
     # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
     p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
+    if FIRST_MAX and NWAVES == 4 and ORDET:
+        p += g.first_max()
     if NWAVES == 8:
         # K1 into the single K buffer behind QK(0) (phase 0 runs QK(1))
         p += [raw('s_nop 3')] + g.kreads(1)
@@ -1651,7 +1685,7 @@ def prologue_persist(g):
     nxt += make_desc(S_NQD, 40, 76, 62, 54, 55, 77)
     lanes_t = [V(f'v_and_b32 v16, 31, v{V_TID}', 16, [V_TID]), V(f'v_bfe_u32 v17, v{V_TID}, 5, 1', 17, [V_TID]),
                V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
-    dec2 = [] if 'nodec2' in PROBE else [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
+    dec2 = [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
     pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + nxt + dec2 + \
         sc['state'] + lanes_t + \
         sc['rows'] + pstamp(PS_V + 4, 'pstA') + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
@@ -1881,11 +1915,28 @@ def masked_tile(g, t, rescue):
     return blk
 
 
-def last_tile(g, t, rescue):
+def last_tile(g, t, rescue, masked=True):
     """Tile t = nt - 1 (position t of the unrolled loop): masked softmax of both blocks, no
-    next-tile reads or DMA, then P.V of block B and the two epilogues."""
-    b = [label(f'.Llast{t}')] + (stamp(STAMP_V + 2) if 'stamps' in PROBE else []) + pstamp(PS_V + 6) + nvrel_insts()
-    b += tile_phases(g, t, masked=True, last=True, rescue=rescue)
+    next-tile reads or DMA, then P.V of block B and the two epilogues. LAST_UNMASKED: the masked
+    form first tests whether any lane's row sees fewer than all 64 keys of the tile and otherwise
+    branches to the unmasked copy (masked=False, .LlastU{t}: key counts that are multiples of 64
+    skip 128 compare/select pairs per block)."""
+    if not masked:
+        b = [label(f'.LlastU{t}')]
+    else:
+        b = [label(f'.Llast{t}')] + (stamp(STAMP_V + 2) if 'stamps' in PROBE else []) + pstamp(PS_V + 6) + nvrel_insts()
+        if LAST_UNMASKED:
+            # masked key offsets reach 59 (32 st + 3 + 24): a lane needs the mask iff NVREL < 60
+            # (no temporaries: the 8-wave form keeps the previous tile's P in V_TMP)
+            nv = sorted({V_NVREL[X] for X in BLOCKS})
+            for i, r in enumerate(nv):
+                b.append(V(f'v_cmp_gt_i32 vcc, 60, v{r}', 'vcc', [r]))
+                last = i == len(nv) - 1
+                b.append(Inst(f's_cbranch_vccz .LlastU{t}' if last else f's_cbranch_vccnz .LlastM{t}', 'br', 4,
+                              rd=['vcc']))
+            if len(nv) > 1:
+                b.append(label(f'.LlastM{t}'))
+    b += tile_phases(g, t, masked=masked, last=True, rescue=rescue)
     if NWAVES == 8:
         b += [mark()] + place(g.pv_sum(par(t), t)[0], [])
         b += [mark()] + g.epilogue('A')
@@ -1934,6 +1985,16 @@ def build(g):
         tiles.append(blk)
     masks = [masked_tile(g, t, rescue) for t in range(U)]
     lasts = [last_tile(g, t, rescue) for t in range(U)]
+    lastsu = [last_tile(g, t, rescue, masked=False) for t in range(U)] if LAST_UNMASKED else []
+
+    def last_paths(t):
+        """The last tile at loop position t: the masked form, and (LAST_UNMASKED) its test then
+        the unmasked copy."""
+        out = [lambda: refs(lasts[t])]
+        if LAST_UNMASKED:
+            ib = next(i for i, x in enumerate(lasts[t]) if x.txt.startswith('s_cbranch_vccz'))
+            out.append(lambda: [(lasts[t], k) for k in range(ib + 1)] + refs(lastsu[t]))
+        return out
     empty = [label('.Lempty')] + sum(([mark()] + g.epilogue(X) for X in BLOCKS), []) + \
             ([raw('s_waitcnt vmcnt(0)'), raw('s_branch .Lseam')] if PERSIST else [raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')])
     # (PERSIST: an empty key set may follow a tail that prefetched its (zero-length) K/V: drain before
@@ -1965,13 +2026,15 @@ def build(g):
         paths.append(lambda: first() + seq(tiles) + seq(tiles))
         for t in range(U):
             paths.append(lambda t=t: first() + seq(tiles) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
-            paths.append(lambda t=t: first() + seq(tiles) + seq(masks) + seq(masks[:t]) + refs(lasts[t]) + nxt() +
-                         seq(tiles))
+            for lp in last_paths(t):
+                paths.append(lambda t=t, lp=lp: first() + seq(tiles) + seq(masks) + seq(masks[:t]) + lp() + nxt() +
+                             seq(tiles))
             # the masked loop (causal band / last tile) entered after only t main tiles of the block's first
             # round, and its last tile reached directly (blocks of fewer than U tiles)
             paths.append(lambda t=t: first() + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
-            paths.append(lambda t=t: first() + seq(tiles[:t]) + [(masks[t], k) for k in range(3)] + refs(lasts[t]) +
-                         nxt() + seq(tiles))
+            for lp in last_paths(t):
+                paths.append(lambda t=t, lp=lp: first() + seq(tiles[:t]) + [(masks[t], k) for k in range(3)] + lp() +
+                             nxt() + seq(tiles))
         paths.append(lambda: first() + refs(empty) + nxt() + seq(tiles))
         paths.append(lambda: refs(pro_a) + [(pb1, k) for k in range(lend + 1)] + refs(end) + refs(pb1) + refs(qload) +
                      refs(pb2) + seq(tiles))
@@ -1990,16 +2053,18 @@ def build(g):
             # main loop -> masked loop entered at position t -> a full masked round
             paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
             # masked loop -> last tile at position t
-            paths.append(lambda t=t: refs(pro) + seq(tiles) + seq(masks) + seq(masks[:t]) + refs(lasts[t]))
+            for lp in last_paths(t):
+                paths.append(lambda t=t, lp=lp: refs(pro) + seq(tiles) + seq(masks) + seq(masks[:t]) + lp())
             # the masked loop entered after only t main tiles (causal band from tile t < U), and its last
             # tile reached directly (fewer than U tiles)
             paths.append(lambda t=t: refs(pro) + seq(tiles[:t]) + seq(masks[t:]) + seq(masks))
-            paths.append(lambda t=t: refs(pro) + seq(tiles[:t]) + [(masks[t], k) for k in range(3)] + refs(lasts[t]))
+            for lp in last_paths(t):
+                paths.append(lambda t=t, lp=lp: refs(pro) + seq(tiles[:t]) + [(masks[t], k) for k in range(3)] + lp())
         paths.append(lambda: refs(pro) + refs(empty))
     # rescale blocks entered from their branch: the 40 instructions before it, the block, the rest
     def resc_path(rb):
         ret = rb[-1].txt.split()[-1]
-        for blk in tiles + masks + lasts + ([tail] if PERSIST else []):
+        for blk in tiles + masks + lasts + lastsu + ([tail] if PERSIST else []):
             for i, x in enumerate(blk):
                 if x.kind == 'br' and x.txt.endswith(f'{ret}:'):
                     lo = max(0, i - 40)
@@ -2009,9 +2074,9 @@ def build(g):
         paths.append(lambda rb=rb: resc_path(rb))
     if PERSIST:
         n = fix_paths(paths)
-        return [pro_a, pb1, qcopy, qload, pb2] + tiles + masks + lasts + [empty, end, done, pb2k, tail] + rescue, n
+        return [pro_a, pb1, qcopy, qload, pb2] + tiles + masks + lasts + lastsu + [empty, end, done, pb2k, tail] + rescue, n
     n = fix_paths(paths)
-    blocks = [pro] + tiles + masks + lasts + [empty, end] + rescue
+    blocks = [pro] + tiles + masks + lasts + lastsu + [empty, end] + rescue
     return blocks, n
 
 
@@ -2105,6 +2170,8 @@ def main():
     ap.add_argument('--kfirst', type=int, default=None, help='K(t+1) reads first in phase 1 (value: first position)')
     ap.add_argument('--prescale', type=int, default=None, help='Q pre-scaled by c, S^T seeded with -m c (D = 64, 4 waves)')
     ap.add_argument('--xphase', type=int, default=None, help='counted lgkmcnt waits across phase marks')
+    ap.add_argument('--fmax', type=int, default=None, help="tile 0's row max sets the starting shift")
+    ap.add_argument('--lastu', type=int, default=None, help='unmasked copy of the last tile')
     ap.add_argument('--mzero', type=int, default=None, help='prologue zeroing by MFMAs (D <= 64)')
     ap.add_argument('--andor', type=int, default=None, help='ORDET: last P word joins the test by v_and_or_b32')
     ap.add_argument('--ptail', type=int, default=None, help='rescale test before the last N MFMAs of its phase')
@@ -2137,7 +2204,11 @@ def main():
     global KFIRST, KFIRST_LO, LGKM_XPHASE, PRESCALE, PHASE_TAIL
     if args.ptail is not None:
         PHASE_TAIL = args.ptail
-    global ORDET_ANDOR, MFMA_ZERO
+    global ORDET_ANDOR, MFMA_ZERO, LAST_UNMASKED, FIRST_MAX
+    if args.fmax is not None:
+        FIRST_MAX = bool(args.fmax)
+    if args.lastu is not None:
+        LAST_UNMASKED = bool(args.lastu)
     if args.mzero is not None:
         MFMA_ZERO = bool(args.mzero)
     if args.andor is not None:

@@ -386,6 +386,10 @@ class Sim:
             if w.vcc.any():
                 w.pc = self.labels[a[0]]
             return
+        if op == 's_cbranch_vccz':
+            if not w.vcc.any():
+                w.pc = self.labels[a[0]]
+            return
         if op.startswith('s_load_dword'):
             n = {'s_load_dword': 1, 's_load_dwordx2': 2, 's_load_dwordx4': 4, 's_load_dwordx16': 16}[op]
             f, i, cnt = self.regs(w, a[0])
@@ -418,6 +422,17 @@ class Sim:
 
     def salu(self, w, op, a):
         d = a[0]
+        if op == 's_cselect_b64':       # 64-bit lane mask (constants -1 / 0 or an SGPR pair)
+            f, lo, n = self.regs(w, d)
+            src = a[1] if w.scc else a[2]
+            m = _RANGE.match(src)
+            if m:
+                v = [int(w.s[int(m.group(2))]), int(w.s[int(m.group(2)) + 1])]
+            else:
+                c = int(src, 0) & 0xFFFFFFFFFFFFFFFF
+                v = [c & 0xFFFFFFFF, c >> 32]
+            w.s[lo], w.s[lo + 1] = v[0] & 0xFFFFFFFF, v[1] & 0xFFFFFFFF
+            return
         x = self.sread(w, a[1]) if len(a) > 1 else 0
         y = self.sread(w, a[2]) if len(a) > 2 else 0
         M = 0xFFFFFFFF
@@ -503,7 +518,12 @@ class Sim:
             return
         if op == 'v_cndmask_b32':
             s0, s1 = self.vread(w, a[1]), self.vread(w, a[2])
-            self.vwrite(w, a[0], np.where(w.vcc, s1, s0).astype(U))
+            mask = w.vcc
+            if len(a) > 3 and a[3] != 'vcc':    # SGPR-pair lane mask
+                _, lo, _ = self.regs(w, a[3])
+                bits = int(w.s[lo]) | (int(w.s[lo + 1]) << 32)
+                mask = np.array([(bits >> l) & 1 for l in range(64)], dtype=bool)
+            self.vwrite(w, a[0], np.where(mask, s1, s0).astype(U))
             return
         if op == 'v_permlane32_swap_b32':
             d, s = self.vread(w, a[0]), self.vread(w, a[1])
@@ -554,6 +574,8 @@ class Sim:
                 r = (src[1].astype(np.int64) - src[0].astype(np.int64)) & 0xFFFFFFFF
             elif op == 'v_min_u32':
                 r = np.minimum(src[0], src[1])
+            elif op == 'v_min_i32':
+                r = np.minimum(src[0].view(np.int32), src[1].view(np.int32)).view(U)
             elif op == 'v_lshl_add_u32':
                 r = ((src[0].astype(np.uint64) << src[1].astype(np.uint64)) + src[2]) & 0xFFFFFFFF
             elif op == 'v_lshl_or_b32':
