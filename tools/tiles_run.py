@@ -40,7 +40,8 @@ def main():
     ap.add_argument("--mode", required=True, choices=["fwd", "bwd"])
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--warm", type=float, default=0.3)
-    ap.add_argument("--impl", default="auto", choices=["auto", "hip"], help="forward kernel family (FaFwdArgs.impl)")
+    ap.add_argument("--impl", default="auto", choices=["auto", "hip", "asm4", "asm8", "asm4p"],
+                    help="forward kernel family (FaFwdArgs.impl)")
     a = ap.parse_args()
     if a.cfg in CFGS:
         B, H, Sq, Sk, D, dts, causal, p, kvpacked = CFGS[a.cfg]
@@ -65,7 +66,7 @@ def main():
 
     def fwd():
         return hip.fwd(q, k, v, cu_q, cu_k, Sq, Sk, p, scale, False, causal, False, None, rng_state=rng,
-                       impl=hip.FA_IMPL_HIP if a.impl == "hip" else hip.FA_IMPL_AUTO)
+                       impl=getattr(hip, "FA_IMPL_" + a.impl.upper()))
 
     if a.mode == "fwd":
         step = fwd
