@@ -71,6 +71,7 @@ V_SEED = {'A': 212, 'B': 228}   # PRESCALE: -m c broadcast over the 16 registers
 KFIRST = True          # phase 1: K(t+1) fragment reads ahead of the V^T reads (D = 64)
 KFIRST_LO = 2          # softmax-stream position of the first K read with KFIRST
 LGKM_XPHASE = True     # counted lgkmcnt waits may count LDS reads of the previous phase
+KSPLIT = 3             # K(t+1) fragment reads moved from phase 1 to the start of phase 2 (D = 64)
 FIRST_MAX = True       # prologue: tile 0's row max sets the starting shift (no rescale at tile 0)
 LAST_UNMASKED = True   # last tile: unmasked copy when every row sees the whole tile
 MFMA_ZERO = True       # prologue: O, row sums, V buffer zeroed by MFMAs of a zero operand (D <= 64)
@@ -844,6 +845,8 @@ class Gen:
         sm = self.softmax('A', masked, rescue)
         self.tail_test(sm, mf)
         side = [] if last else self.kreads(t + 1)
+        if KSPLIT and NBK == 2:
+            side = side[:len(side) - KSPLIT]     # the rest go to phase 2 (kreads_late)
         k_lo = 16
         if NBK == 1:
             # one K buffer: the reads of K(t+1) overwrite what QK_B(t) reads; they go behind its
@@ -883,7 +886,16 @@ class Gen:
         if DMA_P2 and not last:
             dma = self.dma('K', t + 1 + DIST) + dma
         # the V reads go early (two per softmax instruction pair), the DMA pieces in the middle
-        fill = merge(sm, [(i, x) for i, x in zip(spread(len(vr), 1, 56), vr)] +
+        kl = []
+        if KSPLIT and NBK == 2 and not last:
+            # KSPLIT: the last K(t+1) fragment reads (sub-tile 1) open this phase, each issued at
+            # least 3 MFMAs before QK_A(t+1)'s MFMA that reads it
+            rd = self.kreads(t + 1)
+            for j, x in enumerate(rd[len(rd) - KSPLIT:]):
+                x.deadline = max(0, len(rd) - KSPLIT + j - 3)
+                kl.append(x)
+        fill = merge(sm, [(i, x) for i, x in enumerate(kl)] +
+                     [(i, x) for i, x in zip(spread(len(vr), 1, 56), vr)] +
                      [(i, x) for i, x in zip(spread(len(dma), 30, len(sm) - 10), dma)])
         return [mark()] + place(mf, fill)
 
@@ -2170,6 +2182,7 @@ def main():
     ap.add_argument('--kfirst', type=int, default=None, help='K(t+1) reads first in phase 1 (value: first position)')
     ap.add_argument('--prescale', type=int, default=None, help='Q pre-scaled by c, S^T seeded with -m c (D = 64, 4 waves)')
     ap.add_argument('--xphase', type=int, default=None, help='counted lgkmcnt waits across phase marks')
+    ap.add_argument('--ksplit', type=int, default=None, help='K reads moved into phase 2')
     ap.add_argument('--fmax', type=int, default=None, help="tile 0's row max sets the starting shift")
     ap.add_argument('--lastu', type=int, default=None, help='unmasked copy of the last tile')
     ap.add_argument('--mzero', type=int, default=None, help='prologue zeroing by MFMAs (D <= 64)')
@@ -2207,6 +2220,9 @@ def main():
     global ORDET_ANDOR, MFMA_ZERO, LAST_UNMASKED, FIRST_MAX
     if args.fmax is not None:
         FIRST_MAX = bool(args.fmax)
+    global KSPLIT
+    if args.ksplit is not None:
+        KSPLIT = args.ksplit
     if args.lastu is not None:
         LAST_UNMASKED = bool(args.lastu)
     if args.mzero is not None:

@@ -1,4 +1,4 @@
-"""Steady-state driver of one configuration for the per-tile roofline (profiles/r03_tiles_roofline.json).
+"""Steady-state driver of one configuration for the per-tile roofline (profiles/r0N_tiles_roofline.json).
 
     python tools/tiles_run.py --cfg D64 --mode fwd [--launches 200] [--warm 0.3]
 
@@ -24,6 +24,8 @@ from flash_attn import flash_attn_hip as hip  # noqa: E402
 CFGS = {
     "D32": (8, 12, 2048, 2048, 32, "bf16", False, 0.0, False),
     "D64": (8, 12, 2048, 2048, 64, "bf16", False, 0.0, False),
+    "D80": (8, 12, 2048, 2048, 80, "bf16", False, 0.0, False),
+    "D96": (8, 12, 2048, 2048, 96, "bf16", False, 0.0, False),
     "D128": (8, 12, 2048, 2048, 128, "bf16", False, 0.0, False),
     "D128b16": (16, 12, 4096, 4096, 128, "bf16", False, 0.0, False),   # C4's shape, non-causal
     "C2": (8, 12, 512, 512, 64, "fp16", False, 0.0, False),
