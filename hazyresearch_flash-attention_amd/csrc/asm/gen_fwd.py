@@ -71,6 +71,7 @@ V_SEED = {'A': 212, 'B': 228}   # PRESCALE: -m c broadcast over the 16 registers
 KFIRST = True          # phase 1: K(t+1) fragment reads ahead of the V^T reads (D = 64)
 KFIRST_LO = 2          # softmax-stream position of the first K read with KFIRST
 LGKM_XPHASE = True     # counted lgkmcnt waits may count LDS reads of the previous phase
+KSPLIT_LAG = 3         # ... each at least this many MFMAs ahead of its QK MFMA
 KSPLIT = 3             # K(t+1) fragment reads moved from phase 1 to the start of phase 2 (D = 64)
 FIRST_MAX = True       # prologue: tile 0's row max sets the starting shift (no rescale at tile 0)
 LAST_UNMASKED = True   # last tile: unmasked copy when every row sees the whole tile
@@ -892,7 +893,7 @@ class Gen:
             # least 3 MFMAs before QK_A(t+1)'s MFMA that reads it
             rd = self.kreads(t + 1)
             for j, x in enumerate(rd[len(rd) - KSPLIT:]):
-                x.deadline = max(0, len(rd) - KSPLIT + j - 3)
+                x.deadline = max(0, len(rd) - KSPLIT + j - KSPLIT_LAG)
                 kl.append(x)
         fill = merge(sm, [(i, x) for i, x in enumerate(kl)] +
                      [(i, x) for i, x in zip(spread(len(vr), 1, 56), vr)] +
@@ -1698,6 +1699,8 @@ def prologue_persist(g):
     lanes_t = [V(f'v_and_b32 v16, 31, v{V_TID}', 16, [V_TID]), V(f'v_bfe_u32 v17, v{V_TID}, 5, 1', 17, [V_TID]),
                V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
     dec2 = [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
+    if 'dec3' in PROBE:     # timing probe: the current block's decode twice (the price of one decode)
+        dec2 = dec2 + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
     pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + nxt + dec2 + \
         sc['state'] + lanes_t + \
         sc['rows'] + pstamp(PS_V + 4, 'pstA') + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
@@ -2182,6 +2185,7 @@ def main():
     ap.add_argument('--kfirst', type=int, default=None, help='K(t+1) reads first in phase 1 (value: first position)')
     ap.add_argument('--prescale', type=int, default=None, help='Q pre-scaled by c, S^T seeded with -m c (D = 64, 4 waves)')
     ap.add_argument('--xphase', type=int, default=None, help='counted lgkmcnt waits across phase marks')
+    ap.add_argument('--kslag', type=int, default=None, help='KSPLIT reads: MFMAs ahead of their use')
     ap.add_argument('--ksplit', type=int, default=None, help='K reads moved into phase 2')
     ap.add_argument('--fmax', type=int, default=None, help="tile 0's row max sets the starting shift")
     ap.add_argument('--lastu', type=int, default=None, help='unmasked copy of the last tile')
@@ -2223,6 +2227,9 @@ def main():
     global KSPLIT
     if args.ksplit is not None:
         KSPLIT = args.ksplit
+    global KSPLIT_LAG
+    if args.kslag is not None:
+        KSPLIT_LAG = args.kslag
     if args.lastu is not None:
         LAST_UNMASKED = bool(args.lastu)
     if args.mzero is not None:
