@@ -1540,7 +1540,7 @@ def prologue_sections(g):
     p += [S(f's_cmp_eq_u32 s{S_NT}, 0'), raw('s_cbranch_scc1 .Lempty')]
     # K0, K1, V0 (and Q) landed: all but the 8 youngest pieces
     # (8 waves: phase 0 reads K2 as well: K0 K1 V0 K2 landed, all but the 3 youngest pieces)
-    p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else pieces_wait()})')]
+    p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else start_pieces()})')]
     p += [raw('s_barrier')]
     p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
     p += pstamp(PS_V + 4)
@@ -1748,7 +1748,7 @@ def prologue_persist(g):
     qs = ([S('s_cmp_lg_u32 s101, 0'), raw('s_cbranch_scc1 .Lqsdone')] + sc['qscale'] + [label('.Lqsdone')]
           if PRESCALE else [])
     pb2 = [label('.Lqdone'), S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + sc['dma'] + qs + pf + \
-        sc['zero'] + start_with_wait(pieces_wait() + nq)
+        sc['zero'] + start_with_wait(start_pieces() + nq)
     # K0..K3 / V0..V2 came from the previous block's tail: the descriptor sets only walk as the
     # prologue's DMAs would have; younger than K0 K1 V0 are the tail's last 8 pieces, this
     # block's 2 x 5 O / LSE stores per wave and the next Q's loads
@@ -1760,6 +1760,7 @@ def prologue_persist(g):
 
 N_STORES = 10         # LSE + O stores per wave of the epilogue (D = 64: 2 x (1 + 4); set_persist)
 PERSIST_Q = True      # persistent form: next-block Q prefetch (D = 64 only)
+BAR2 = False          # main loop: one barrier per two tiles (needs R >= 6, DIST >= 3, even unroll)
 PERSIST_KV = True     # persistent form: the tail streams the next block's K0..K3 / V0..V2
 
 
@@ -1905,6 +1906,19 @@ def tile_vmcnt():
     return 2 * NP * (DIST - 2) if NWAVES == 8 else pieces_wait()
 
 
+def bar2_vmcnt():
+    """BAR2 (main loop barrier after odd tiles only): the barrier after tile t publishes the data of
+    tiles t+1 and t+2 (K(t+3), V(t+2) and older): the DMAs of the last DIST - 2 tiles may stay in
+    flight. Slot reuse needs a ring of 6 (a fast wave may lead by up to two tiles)."""
+    return min(2 * NP, 4) * (DIST - 2)
+
+
+def start_pieces():
+    """DMA pieces that may still be in flight at the prologue's barrier: pieces_wait(), or with
+    BAR2 one tile fewer (no barrier after tile 0: tile 1's K(2), V(1) must be published here)."""
+    return pieces_wait() - (min(2 * NP, 4) if BAR2 else 0)
+
+
 def pieces_wait():
     """4-wave form: DMA pieces that may stay in flight when the next tile starts: the last DIST - 1
     tiles' (2 NP each; D = 32 has NP = 1 and needs exactly this). At D = 128 (NP = 4) the stricter
@@ -1992,8 +2006,8 @@ def build(g):
             blk += g.phase2(t, rescue=rescue)
             if DUMP and DUMP[0] == 'p2' and t == 0:
                 blk += dump_block(DUMP[1])
-        if 'nobar' not in PROBE:
-            blk += [raw(f's_waitcnt vmcnt({tile_vmcnt()})'), raw('s_barrier')]
+        if 'nobar' not in PROBE and (not BAR2 or t % 2 == 1):
+            blk += [raw(f's_waitcnt vmcnt({bar2_vmcnt() if BAR2 else tile_vmcnt()})'), raw('s_barrier')]
         blk += [S(f's_add_u32 s{S_J}, s{S_J}, 1')]
         if t == U - 1:
             blk.append(raw('s_branch .Lloop'))
@@ -2174,6 +2188,8 @@ def main():
     ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')
     ap.add_argument('--probe', default='', help='timing-only variant switches, comma separated')
     ap.add_argument('--ring', type=int, default=None)
+    ap.add_argument('--bar2', type=int, default=None, help='main-loop barrier after odd tiles only (with --ring 6 --dist 4)')
+    ap.add_argument('--kvtail', type=int, default=None, help='persistent form: stream the next block K/V in the tail')
     ap.add_argument('--dist', type=int, default=None)
     ap.add_argument('--vp1', type=int, default=None)
     ap.add_argument('--smpipe', type=int, default=None)
@@ -2202,6 +2218,12 @@ def main():
     global VREADS_P1, SM_PIPE
     if args.ring or args.dist:
         set_geometry(args.ring or R, args.dist or DIST)
+    global BAR2, PERSIST_KV
+    if args.bar2 is not None:
+        BAR2 = bool(args.bar2)
+        assert not BAR2 or (R >= 6 and DIST >= 3 and U % 2 == 0)
+    if args.kvtail is not None:
+        PERSIST_KV = bool(args.kvtail)
     if args.vp1 is not None:
         VREADS_P1 = bool(args.vp1)
     if args.smpipe is not None:
