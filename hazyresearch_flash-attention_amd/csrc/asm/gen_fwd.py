@@ -148,7 +148,24 @@ def rqn(base, n=4):
     return rv(base, n) if QL_VGPR else ra(base, n)
 
 
+# LDS ring per form: (slots, DMA distance, one barrier per two tiles, persistent K/V tail). D <= 64
+# (4 waves): 6 slots (96 KiB), distance 4, a barrier after odd tiles only (a fast wave leads by up
+# to two tiles, so a slot is rewritten two tiles after its last read) and no K/V tail (its seam
+# saving measured ~0 once tile 0 stopped taking the rescale; the tail needs nt % R == 0). D = 128
+# (32 KiB per slot) and the 8-wave form keep 4 slots, distance 3, a barrier per tile.
+GEOMETRY = {(64, 4): (6, 4, True, False), (32, 4): (6, 4, True, False),
+            (128, 4): (4, 3, False, True), (64, 8): (4, 3, False, True)}
+
+
 def configure(hd, waves=4):
+    """The head-dim tile's register map (configure_layout), then its ring geometry (GEOMETRY)."""
+    global BAR2, PERSIST_KV
+    configure_layout(hd, waves)
+    r, dist, BAR2, PERSIST_KV = GEOMETRY[(hd, waves)]
+    set_geometry(r, dist)
+
+
+def configure_layout(hd, waves=4):
     """Head-dim tile. 64: the layout above (head_dim in (32, 64]). 128 (head_dim == 128): twice the
     k-steps and d-blocks, single K / V^T fragment buffers (the K reads of tile j+1 follow the last
     QK_B(j) MFMA, the V^T reads of tile j follow PV_B(j-1), one phase earlier), Q / O offsets as
@@ -1659,7 +1676,7 @@ def product_prescale(dtype, hd, waves, persist):
     return hd == 64 and waves == 4 and persist and PRESCALE_PRODUCT.get(dtype, False)
 
 
-PRESCALE_PRODUCT = {'bf16': True, 'f16': False}
+PRESCALE_PRODUCT = {'bf16': True, 'f16': True}
 
 
 def set_persist(on):
@@ -1994,7 +2011,7 @@ def build(g):
         if t == 0:
             blk.append(raw('.p2align 6'))
             blk.append(label('.Lloop'))
-        if PERSIST and t == 0:
+        if PERSIST and PERSIST_KV and t == 0:
             blk += [S(f's_cmp_eq_u32 s{S_J}, s{S_TAIL}'), raw('s_cbranch_scc1 .Ltail')]
         blk += [S(f's_cmp_ge_u32 s{S_J}, s{S_MSTART}'), raw(f's_cbranch_scc1 .Lmask{t}')]
         if NWAVES == 8:
@@ -2039,7 +2056,7 @@ def build(g):
         done = [label('.Ldone'), raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
         # a block past its sequence: the previous tail's DMAs must land before this slot reuse
         end.insert(1, raw('s_waitcnt vmcnt(0)'))
-        tail = tail_blocks(g, rescue)
+        tail = tail_blocks(g, rescue) if PERSIST_KV else []
     # control-flow paths for the hazard pass
     paths = []
     def seq(blks):
@@ -2067,15 +2084,16 @@ def build(g):
         paths.append(lambda: first() + refs(empty) + nxt() + seq(tiles))
         paths.append(lambda: refs(pro_a) + [(pb1, k) for k in range(lend + 1)] + refs(end) + refs(pb1) + refs(qload) +
                      refs(pb2) + seq(tiles))
-        itail = next(i for i, x in enumerate(tiles[0]) if x.txt.endswith('.Ltail'))
         ikv = next(i for i, x in enumerate(pb2) if x.txt.endswith('.Lkvpf'))
-        for_tail = lambda: first() + seq(tiles) + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
-        paths.append(lambda: for_tail() + nxt_from_tail() + seq(tiles) + seq(tiles))
-        # a block of exactly 4 tiles enters the tail at its first tile
-        tail_now = lambda: first() + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
-        paths.append(lambda: tail_now() + nxt_from_tail() + seq(tiles) + seq(tiles))
-        paths.append(lambda: for_tail() + nxt_from_tail() + [(tiles[0], k) for k in range(itail + 1)] + refs(tail))
         nxt_from_tail = lambda: seam() + refs(pb1) + refs(qsel) + [(pb2, k) for k in range(ikv + 1)] + refs(pb2k)
+        if PERSIST_KV:
+            itail = next(i for i, x in enumerate(tiles[0]) if x.txt.endswith('.Ltail'))
+            for_tail = lambda: first() + seq(tiles) + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
+            paths.append(lambda: for_tail() + nxt_from_tail() + seq(tiles) + seq(tiles))
+            # a block of exactly 4 tiles enters the tail at its first tile
+            tail_now = lambda: first() + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
+            paths.append(lambda: tail_now() + nxt_from_tail() + seq(tiles) + seq(tiles))
+            paths.append(lambda: for_tail() + nxt_from_tail() + [(tiles[0], k) for k in range(itail + 1)] + refs(tail))
     else:
         paths.append(lambda: refs(pro) + seq(tiles) + seq(tiles))
         for t in range(U):
@@ -2093,7 +2111,7 @@ def build(g):
     # rescale blocks entered from their branch: the 40 instructions before it, the block, the rest
     def resc_path(rb):
         ret = rb[-1].txt.split()[-1]
-        for blk in tiles + masks + lasts + lastsu + ([tail] if PERSIST else []):
+        for blk in tiles + masks + lasts + lastsu + ([tail] if PERSIST and tail else []):
             for i, x in enumerate(blk):
                 if x.kind == 'br' and x.txt.endswith(f'{ret}:'):
                     lo = max(0, i - 40)
@@ -2103,7 +2121,8 @@ def build(g):
         paths.append(lambda rb=rb: resc_path(rb))
     if PERSIST:
         n = fix_paths(paths)
-        return [pro_a, pb1, qcopy, qload, pb2] + tiles + masks + lasts + lastsu + [empty, end, done, pb2k, tail] + rescue, n
+        return [pro_a, pb1, qcopy, qload, pb2] + tiles + masks + lasts + lastsu + [empty, end, done, pb2k] + \
+            ([tail] if tail else []) + rescue, n
     n = fix_paths(paths)
     blocks = [pro] + tiles + masks + lasts + lastsu + [empty, end] + rescue
     return blocks, n
