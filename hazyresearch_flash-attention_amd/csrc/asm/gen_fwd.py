@@ -1724,9 +1724,16 @@ def prologue_persist(g):
     qcopy = [Inst(f'v_accvgpr_write_b32 a{A_Q[X] + r}, v{V_QN + 16 * xi + r}', 'accw',
                   rd=[f'v{V_QN + 16 * xi + r}'], wr=[f'a{A_Q[X] + r}'])
              for xi, X in enumerate(BLOCKS) for r in range(16)] + [raw('s_branch .Lqdone')]
-    if PRESCALE:    # the prefetched Q is scaled on its way into the AGPRs (no AGPR pass at .Lqdone)
-        qcopy = q_prescale(g, src=[(V_QN + 16 * xi + r, A_Q[X] + r) for xi, X in enumerate(BLOCKS)
-                                   for r in range(16)]) + pstamp(PS_V + 4, 'pstB') + [raw('s_branch .Lqdone')]
+    qcopy_late = []
+    if PRESCALE:
+        # the prefetched Q is scaled on its way into the AGPRs (no AGPR pass at .Lqdone), after this
+        # block's first DMAs are issued: its ~800 cycles run under their latency (QCOPY_LATE)
+        qc = q_prescale(g, src=[(V_QN + 16 * xi + r, A_Q[X] + r) for xi, X in enumerate(BLOCKS)
+                                for r in range(16)]) + pstamp(PS_V + 4, 'pstB')
+        if QCOPY_LATE:
+            qcopy, qcopy_late = [raw('s_branch .Lqdone')], qc
+        else:
+            qcopy = qc + [raw('s_branch .Lqdone')]
     if not PERSIST_Q:
         qcopy = []
     qload = [label('.Lqload')] + sc['qload']
@@ -1764,8 +1771,21 @@ def prologue_persist(g):
     # the first wait waits for Q, K0, K1, V0: younger are K2 V1 K3 V2 (8 pieces) and the next Q's loads
     qs = ([S('s_cmp_lg_u32 s101, 0'), raw('s_cbranch_scc1 .Lqsdone')] + sc['qscale'] + [label('.Lqsdone')]
           if PRESCALE else [])
+    qcb = qfb = None
+    if qcopy_late:
+        # later blocks: the prefetched Q, scaled (qcb); the first block, s101 == 0: Q~ in place (qfb).
+        # Separate blocks, so that the hazard pass walks each on its own path (build: pb2 parts)
+        qs = [S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqfirst')]
+        qcb = qcopy_late + [raw('s_branch .Lqsdone')]
+        qfb = [label('.Lqfirst')] + sc['qscale']
     pb2 = [label('.Lqdone'), S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + sc['dma'] + qs + pf + \
         sc['zero'] + start_with_wait(start_pieces() + nq)
+    if qcb is not None:
+        # pb2 as [head up to the branch, the copy, the first-block scale, the rest from .Lqsdone]
+        i = len(pb2) - len(pf) - len(sc['zero']) - len(sc['start'])
+        pb2 = [pb2[:i], qcb, qfb, [label('.Lqsdone')] + pb2[i:]]
+    else:
+        pb2 = [pb2]
     # K0..K3 / V0..V2 came from the previous block's tail: the descriptor sets only walk as the
     # prologue's DMAs would have; younger than K0 K1 V0 are the tail's last 8 pieces, this
     # block's 2 x 5 O / LSE stores per wave and the next Q's loads
@@ -1777,6 +1797,7 @@ def prologue_persist(g):
 
 N_STORES = 10         # LSE + O stores per wave of the epilogue (D = 64: 2 x (1 + 4); set_persist)
 PERSIST_Q = True      # persistent form: next-block Q prefetch (D = 64 only)
+QCOPY_LATE = True     # persistent PRESCALE: the next-Q copy + scale after the block's first DMAs
 BAR2 = False          # main loop: one barrier per two tiles (needs R >= 6, DIST >= 3, even unroll)
 PERSIST_KV = True     # persistent form: the tail streams the next block's K0..K3 / V0..V2
 
@@ -2000,7 +2021,7 @@ def build(g):
     rescue = []
     if PERSIST:
         pro_a, pb1, qcopy, qload, pb2, pb2k = prologue_persist(g)
-        pro = pro_a + pb1 + qload + pb2       # (only for the DUMP hook below)
+        pro = pro_a + pb1 + qload + sum(pb2, [])       # (only for the DUMP hook below)
     else:
         pro = stamp_entry() + prologue(g)
     if DUMP and DUMP[0] == 'pro':
@@ -2062,12 +2083,15 @@ def build(g):
     def seq(blks):
         return sum((refs(b) for b in blks), [])
     if PERSIST:
-        first = lambda: refs(pro_a) + refs(pb1) + refs(qload) + refs(pb2)
+        # pb2 parts: one block, or [head, next-Q copy, first-block Q scale, rest] (QCOPY_LATE)
+        p2_first = lambda: sum((refs(b) for b in (pb2[:1] + pb2[2:] if len(pb2) > 1 else pb2)), [])
+        p2_next = lambda: sum((refs(b) for b in (pb2[:2] + pb2[3:] if len(pb2) > 1 else pb2)), [])
+        first = lambda: refs(pro_a) + refs(pb1) + refs(qload) + p2_first()
         qsel = qcopy if PERSIST_Q else qload
         # a finished block reaches the next one at .Lseam (the .Lend entry above it drains vmcnt, .Lseam does not)
         iseam = next(i for i, x in enumerate(end) if x.kind == 'label' and x.txt.startswith('.Lseam'))
         seam = lambda: [(end, k) for k in range(iseam, len(end))]
-        nxt = lambda: seam() + refs(pb1) + refs(qsel) + refs(pb2)
+        nxt = lambda: seam() + refs(pb1) + refs(qsel) + p2_next()
         lend = next(i for i, x in enumerate(pb1) if x.txt.endswith('.Lend'))
         paths.append(lambda: first() + seq(tiles) + seq(tiles))
         for t in range(U):
@@ -2083,9 +2107,9 @@ def build(g):
                              nxt() + seq(tiles))
         paths.append(lambda: first() + refs(empty) + nxt() + seq(tiles))
         paths.append(lambda: refs(pro_a) + [(pb1, k) for k in range(lend + 1)] + refs(end) + refs(pb1) + refs(qload) +
-                     refs(pb2) + seq(tiles))
-        ikv = next(i for i, x in enumerate(pb2) if x.txt.endswith('.Lkvpf'))
-        nxt_from_tail = lambda: seam() + refs(pb1) + refs(qsel) + [(pb2, k) for k in range(ikv + 1)] + refs(pb2k)
+                     p2_first() + seq(tiles))
+        ikv = next(i for i, x in enumerate(pb2[0]) if x.txt.endswith('.Lkvpf'))
+        nxt_from_tail = lambda: seam() + refs(pb1) + refs(qsel) + [(pb2[0], k) for k in range(ikv + 1)] + refs(pb2k)
         if PERSIST_KV:
             itail = next(i for i, x in enumerate(tiles[0]) if x.txt.endswith('.Ltail'))
             for_tail = lambda: first() + seq(tiles) + [(tiles[0], k) for k in range(itail + 1)] + refs(tail)
@@ -2121,7 +2145,7 @@ def build(g):
         paths.append(lambda rb=rb: resc_path(rb))
     if PERSIST:
         n = fix_paths(paths)
-        return [pro_a, pb1, qcopy, qload, pb2] + tiles + masks + lasts + lastsu + [empty, end, done, pb2k] + \
+        return [pro_a, pb1, qcopy, qload] + pb2 + tiles + masks + lasts + lastsu + [empty, end, done, pb2k] + \
             ([tail] if tail else []) + rescue, n
     n = fix_paths(paths)
     blocks = [pro] + tiles + masks + lasts + lastsu + [empty, end] + rescue
@@ -2207,6 +2231,7 @@ def main():
     ap.add_argument('--dump', default=None, help='debug: point:reg,reg,... (pro|p1|p2)')
     ap.add_argument('--probe', default='', help='timing-only variant switches, comma separated')
     ap.add_argument('--ring', type=int, default=None)
+    ap.add_argument('--qlate', type=int, default=None, help='persistent: Q copy + scale after the first DMAs')
     ap.add_argument('--bar2', type=int, default=None, help='main-loop barrier after odd tiles only (with --ring 6 --dist 4)')
     ap.add_argument('--kvtail', type=int, default=None, help='persistent form: stream the next block K/V in the tail')
     ap.add_argument('--dist', type=int, default=None)
@@ -2237,7 +2262,9 @@ def main():
     global VREADS_P1, SM_PIPE
     if args.ring or args.dist:
         set_geometry(args.ring or R, args.dist or DIST)
-    global BAR2, PERSIST_KV
+    global BAR2, PERSIST_KV, QCOPY_LATE
+    if args.qlate is not None:
+        QCOPY_LATE = bool(args.qlate)
     if args.bar2 is not None:
         BAR2 = bool(args.bar2)
         assert not BAR2 or (R >= 6 and DIST >= 3 and U % 2 == 0)
