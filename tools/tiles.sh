@@ -1,5 +1,5 @@
 #!/bin/bash
-# Per-tile roofline evidence for round 3 (profiles/r03_tiles_roofline.json):
+# Per-tile roofline evidence (profiles/r0N_tiles_roofline.json; round 4 adds D80 and D96):
 # for each configuration and mode (forward-only loop, backward-only loop) one steady-state
 # kernel-trace pass (>= 0.3 s warm-up, then 200 timed calls, event time printed by the driver)
 # and three short PMC passes (FETCH_SIZE; WRITE_SIZE; MFMA busy + GRBM + MFMA/VALU instruction

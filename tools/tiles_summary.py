@@ -1,6 +1,6 @@
-"""Summarise tools/tiles.sh into profiles/r03_tiles_roofline.json.
+"""Summarise tools/tiles.sh into profiles/r0N_tiles_roofline.json.
 
-    python tools/tiles_summary.py <outdir> > profiles/r03_tiles_roofline.json
+    python tools/tiles_summary.py <outdir> > profiles/r0N_tiles_roofline.json
 
 Per configuration and mode (fwd-only loop / bwd-only loop):
   * per kernel: average duration over the timed (last) dispatches of the kernel-trace pass,
