@@ -154,13 +154,19 @@ def rqn(base, n=4):
 # saving measured ~0 once tile 0 stopped taking the rescale; the tail needs nt % R == 0). D = 128
 # (32 KiB per slot) and the 8-wave form keep 4 slots, distance 3, a barrier per tile.
 GEOMETRY = {(64, 4): (6, 4, True, False), (32, 4): (6, 4, True, False),
-            (128, 4): (4, 3, False, True), (64, 8): (4, 3, False, True)}
+            (128, 4): (4, 3, False, True), (96, 4): (4, 3, False, True), (64, 8): (4, 3, False, True)}
+D_NAME = 64            # the tile named in the kernel symbol (96: the D = 128 layout computing 96 columns)
 
 
 def configure(hd, waves=4):
-    """The head-dim tile's register map (configure_layout), then its ring geometry (GEOMETRY)."""
-    global BAR2, PERSIST_KV
-    configure_layout(hd, waves)
+    """The head-dim tile's register map (configure_layout), then its ring geometry (GEOMETRY).
+    hd = 96: the D = 128 layout (LDS rows, registers, DMA) with the QK k-steps and PV d-blocks of
+    96 columns only (NKS 6, NDT 3); head_dim 80 zeroes Q's k-step 5 and drops the O chunk 80..95."""
+    global BAR2, PERSIST_KV, NKS, NDT, D_NAME
+    configure_layout(128 if hd == 96 else hd, waves)
+    D_NAME = hd
+    if hd == 96:
+        NKS, NDT = 6, 3
     r, dist, BAR2, PERSIST_KV = GEOMETRY[(hd, waves)]
     set_geometry(r, dist)
 
@@ -341,7 +347,7 @@ class Gen:
         self.cvt = 'v_cvt_pk_bf16_f32' if dtype == 'bf16' else 'v_cvt_pk_f16_f32'
         self.one2 = 0x3F803F80 if dtype == 'bf16' else 0x3C003C00
         self.nlabel = 0
-        self.name = f'fa_fwd_d{D}{"w8" if NWAVES == 8 else ""}{"p" if PERSIST else ""}_{dtype}_asm'
+        self.name = f'fa_fwd_d{D_NAME}{"w8" if NWAVES == 8 else ""}{"p" if PERSIST else ""}_{dtype}_asm'
 
     def lab(self, stem):
         self.nlabel += 1
@@ -840,6 +846,12 @@ class Gen:
                     oreg, oimm = V_OOFF[X], f' offset:{16 * (4 * dt + g)}'
                 else:
                     oreg, oimm = V_OOFF[X] + dt * 2 + gi, ''
+                if D_NAME == 96 and dt == 2 and g == 2:
+                    # columns 80..95: dropped for head_dim 80 (the offset pushed past num_records)
+                    e += [Inst('s_cmp_gt_u32 s74, 80', 'salu', 2, rd=['s74']),
+                          Inst('s_cselect_b32 s96, 0, 0x80000000', 'salu', 2, wr=['s96']),
+                          V(f'v_or_b32 v{T + 4}, s96, v{oreg}', T + 4, [oreg])]
+                    oreg = T + 4
                 if 'noepi' not in PROBE:
                     e.append(Inst(f'buffer_store_dwordx4 {vs(Wb, 4)}, v{oreg}, s[{S_OD}:{S_OD + 3}], 0 offen{oimm}',
                                   'vstore', 8, rd=rv(Wb, 4) + [f'v{oreg}']))
@@ -1493,10 +1505,19 @@ def prologue_sections(g):
         p += [Inst(f'v_accvgpr_write_b32 a{A_ONES + r}, v51', 'accw', rd=['v51'], wr=[f'a{A_ONES + r}']) for r in range(4)]
     # Q fragments ('nopro' timing probe: no Q loads and no first DMAs, the prologue burst's price)
     p.append(sec('qload'))
+    if D_NAME == 96 and 'nopro' not in PROBE:
+        # head_dim 80: Q's k-step 5 (columns 80..95: another head's, or past the tensor) loads
+        # through an offset pushed past num_records (zeros)
+        p += [Inst('s_cmp_gt_u32 s74, 80', 'salu', 2, rd=['s74']),
+              Inst('s_cselect_b32 s96, 0, 0x80000000', 'salu', 2, wr=['s96'])]
+        p += [V(f'v_or_b32 v{V_P["A"] + 2 + i}, s96, v{qoff[X]}', V_P['A'] + 2 + i, [qoff[X]])
+              for i, X in enumerate(BLOCKS)]
     for X in ([] if 'nopro' in PROBE else BLOCKS):
         for ks in range(NKS):
             q = A_Q[X] + 4 * ks
             qr, qi = (qoff[X], f' offset:{32 * ks}') if O_BASE else (qoff[X] + ks, '')
+            if D_NAME == 96 and ks == 5:
+                qr = V_P['A'] + 2 + BLOCKS.index(X)
             p.append(Inst(f'buffer_load_dwordx4 {rq(q)}, v{qr}, s[{S_QD}:{S_QD + 3}], 0 offen{qi}', 'vload', 8,
                           rd=[f'v{qr}'], wr=rqn(q)))
     # first DMAs: K0, [K1 V0], [K2 V1], [K3 V2] (tile t of the loop issues K(t+1+DIST), V(t+DIST))
@@ -2222,7 +2243,7 @@ def expand_regs(spec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'f16'])
-    ap.add_argument('--hd', type=int, default=64, choices=[32, 64, 128], help='head-dim tile')
+    ap.add_argument('--hd', type=int, default=64, choices=[32, 64, 96, 128], help='head-dim tile')
     ap.add_argument('--waves', type=int, default=4, choices=[4, 8], help='waves per workgroup (8: D = 64 only)')
     ap.add_argument('--prio4', type=int, default=None, help='8 waves: s_setprio 1 for waves 4-7')
     ap.add_argument('--persist', type=int, default=0, help='persistent workgroups: next-block K/V tail (and next-Q prefetch at D = 64), 4 waves')

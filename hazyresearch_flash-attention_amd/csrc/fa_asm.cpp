@@ -39,6 +39,14 @@ extern const unsigned char fa_asm_fwd_d128p_bf16[];
 extern const unsigned long fa_asm_fwd_d128p_bf16_size;
 extern const unsigned char fa_asm_fwd_d128p_f16[];
 extern const unsigned long fa_asm_fwd_d128p_f16_size;
+extern const unsigned char fa_asm_fwd_d96_bf16[];
+extern const unsigned long fa_asm_fwd_d96_bf16_size;
+extern const unsigned char fa_asm_fwd_d96_f16[];
+extern const unsigned long fa_asm_fwd_d96_f16_size;
+extern const unsigned char fa_asm_fwd_d96p_bf16[];
+extern const unsigned long fa_asm_fwd_d96p_bf16_size;
+extern const unsigned char fa_asm_fwd_d96p_f16[];
+extern const unsigned long fa_asm_fwd_d96p_f16_size;
 }
 
 namespace fa {
@@ -83,8 +91,8 @@ constexpr int kMaxDev = 64;
 constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
 
 // kernels: [form (0: D=64, 1: D=128, 2: D=64 two waves per SIMD, 3: D=64 persistent, 4: D=128
-// persistent) * 2 + dtype (0: bf16, 1: f16)]
-constexpr int kNumFns = 10;
+// persistent, 5: D=96, 6: D=96 persistent) * 2 + dtype (0: bf16, 1: f16)]
+constexpr int kNumFns = 14;
 struct DevFns {
     hipModule_t mod[kNumFns] = {};
     hipFunction_t fn[kNumFns] = {};
@@ -103,12 +111,16 @@ hipError_t load_all(DevFns &d) {
                                               fa_asm_fwd_d128_bf16,  fa_asm_fwd_d128_f16,
                                               fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16,
                                               fa_asm_fwd_d64p_bf16,  fa_asm_fwd_d64p_f16,
-                                              fa_asm_fwd_d128p_bf16, fa_asm_fwd_d128p_f16};
+                                              fa_asm_fwd_d128p_bf16, fa_asm_fwd_d128p_f16,
+                                              fa_asm_fwd_d96_bf16,   fa_asm_fwd_d96_f16,
+                                              fa_asm_fwd_d96p_bf16,  fa_asm_fwd_d96p_f16};
     static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
                                                "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
                                                "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
                                                "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
-                                               "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm"};
+                                               "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm",
+                                               "fa_fwd_d96_bf16_asm",   "fa_fwd_d96_f16_asm",
+                                               "fa_fwd_d96p_bf16_asm",  "fa_fwd_d96p_f16_asm"};
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     const bool exchanged = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
     hipError_t e = hipSuccess;
@@ -149,8 +161,10 @@ bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
     if (a.impl == FA_IMPL_HIP) return false;
     if (bm.mask || a.p_dropout > 0.f || a.rot_cos) return false;
     // D = 64 tile: head_dim in (32, 64] (zero-padded); D = 128 tile: head_dim == 128 only (its Q loads
-    // and O stores address whole rows from one base)
-    if (!((a.head_dim > 32 && a.head_dim <= 64) || a.head_dim == 128)) return false;
+    // and O stores address whole rows from one base); D = 96 tile (the D = 128 layout computing 96
+    // columns): head_dim 96, or 80 (k-step 5 of Q loaded as zeros, O columns 80..95 not stored)
+    if (!((a.head_dim > 32 && a.head_dim <= 64) || a.head_dim == 80 || a.head_dim == 96 || a.head_dim == 128))
+        return false;
     if (a.max_seqlen_q <= 0) return false;
     // byte strides must fit the kernel's 32-bit row strides; the magic divisions are exact for
     // n * d <= 2^30 (n < workgroups, d = q-blocks per head or heads)
@@ -210,8 +224,8 @@ static int asm_form(const FaFwdArgs &a, int *pgrid) {
     const bool w8 = use_w8(a);
     const uint32_t nqb0 = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
     *pgrid = w8 ? 0 : persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
-    const bool d128 = a.head_dim > 64;
-    return w8 ? 2 : *pgrid ? (d128 ? 4 : 3) : (d128 ? 1 : 0);
+    const bool d128 = a.head_dim > 96, d96 = a.head_dim > 64 && !d128;
+    return w8 ? 2 : *pgrid ? (d128 ? 4 : d96 ? 6 : 3) : (d128 ? 1 : d96 ? 5 : 0);
 }
 
 const char *asm_kernel_name(const FaFwdArgs &a) {
@@ -219,7 +233,9 @@ const char *asm_kernel_name(const FaFwdArgs &a) {
                                                "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
                                                "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
                                                "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
-                                               "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm"};
+                                               "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm",
+                                               "fa_fwd_d96_bf16_asm",   "fa_fwd_d96_f16_asm",
+                                               "fa_fwd_d96p_bf16_asm",  "fa_fwd_d96p_f16_asm"};
     int pgrid = 0;
     return names[2 * asm_form(a, &pgrid) + (a.dtype == FA_DTYPE_BF16 ? 0 : 1)];
 }

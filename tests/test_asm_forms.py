@@ -127,6 +127,20 @@ def test_asm_form_forward_d128(form, seqlen_q, seqlen_k):
         run_case("separate", 6, seqlen_q, seqlen_k, 8, 128, torch.bfloat16, False, 0.0, grad=False, seed=seqlen_k)
 
 
+@pytest.mark.parametrize("form", ["ASM4", "ASM4P"])
+@pytest.mark.parametrize("d", [80, 96])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("seqlen_q,seqlen_k", [(257, 513), (1025, 1100)])
+def test_asm_form_forward_d96(form, d, causal, seqlen_q, seqlen_k):
+    """The D = 96 tile (D = 128 layout computing 96 columns) at head_dim 96 and 80 (Q's k-step 5
+    loaded as zeros, O columns 80..95 never stored), one-block and persistent."""
+    hip = _hip()
+    assert hip.fwd_kernel_name(6, 8, d, seqlen_q, seqlen_k, torch.bfloat16,
+                               impl=getattr(hip, f"FA_IMPL_{form}")).startswith("fa_fwd_d96")
+    with hip.force_impl(getattr(hip, f"FA_IMPL_{form}")):
+        run_case("separate", 6, seqlen_q, seqlen_k, 8, d, torch.bfloat16, causal, 0.0, grad=False, seed=seqlen_k + d)
+
+
 @pytest.mark.parametrize("d", [64, 128])
 def test_asm_persistent_empty_key_set_after_tail(d):
     """the persistent form's .Lempty path right after a block that took the K/V tail

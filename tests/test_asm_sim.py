@@ -44,8 +44,9 @@ def _kernel(dtype, hd=64, waves=4, persist=False, prescale=None):
     return _TXT[key]
 
 
-def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4, grid=None, prescale=None):
-    """grid: the persistent form's workgroup count (each walks blocks L, L + grid, ...)."""
+def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4, grid=None, prescale=None, hd=None):
+    """grid: the persistent form's workgroup count (each walks blocks L, L + grid, ...); hd: the
+    tile (default: the one fa_asm.cpp picks for head_dim D)."""
     rng = np.random.default_rng(seed)
     cv = asm_sim.bf16_bits if dtype == "bf16" else asm_sim.f16_bits
     B, tq, tk = len(lens_q), sum(lens_q), sum(lens_k)
@@ -77,7 +78,8 @@ def _run(lens_q, lens_k, H, D, dtype, scale=None, seed=0, causal=False, waves=4,
     if grid:
         karg += struct.pack("<2I", grid, 0)
     pa = mem.alloc(np.frombuffer(karg, np.uint8))
-    hd = 128 if D > 64 else 64 if D > 32 else 32
+    if hd is None:
+        hd = 128 if D > 96 else 96 if D > 64 else 64 if D > 32 else 32
     if prescale is None:
         prescale = gen_fwd.product_prescale(dtype, hd, waves, bool(grid))
     asm_sim.Sim(_kernel(dtype, hd, waves, bool(grid), prescale), dtype).run(
@@ -262,7 +264,8 @@ def test_asm_forward_prescaled_in_simulator(lens_q, lens_k, H, D, grid, dtype, c
 def _run_text(txt, lens_q, lens_k, H, D, dtype, mode="lazy"):
     """_run with a given kernel text (the product kernel cache bypassed)."""
     saved = dict(_TXT)
-    hd = 128 if D > 64 else 64 if D > 32 else 32
+    if hd is None:
+        hd = 128 if D > 96 else 96 if D > 64 else 64 if D > 32 else 32
     _TXT.clear()
     _TXT[(dtype, hd, 4, False, gen_fwd.product_prescale(dtype, hd, 4, False))] = txt
     orig = asm_sim.Sim.__init__
@@ -312,3 +315,15 @@ def test_simulator_catches_a_missing_wait_state():
     bad = "\n".join(lines[:i - 1] + lines[i:])
     with pytest.raises(asm_sim.HazardError):
         _run_text(bad, [130], [200], 1, 64, "bf16")
+
+
+@pytest.mark.parametrize("lens_q,lens_k,H,D,grid,causal", [
+    ([300, 200], [512, 256], 2, 96, None, False),    # one-block, two sequences
+    ([130], [300], 2, 80, None, False),              # head_dim 80: Q k-step 5 zeroed, O columns 80..95 dropped
+    ([257, 100], [700, 190], 2, 80, None, True),     # causal band
+    ([300, 200], [512, 256], 2, 96, 2, False),       # persistent, K/V tail into the next block
+    ([300, 40], [640, 0], 2, 80, 3, False),          # persistent, empty key set, head_dim 80
+])
+def test_asm_forward_d96_in_simulator(lens_q, lens_k, H, D, grid, causal):
+    """The D = 96 tile (D = 128 layout, 6 k-steps and 3 d-blocks) at head_dim 96 and 80."""
+    _run(lens_q, lens_k, H, D, "bf16", causal=causal, grid=grid, hd=96)

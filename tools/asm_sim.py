@@ -478,6 +478,9 @@ class Sim:
         elif op == 's_cmp_lt_u32':
             w.scc = self.sread(w, a[0]) < x
             return
+        elif op == 's_cmp_gt_u32':
+            w.scc = self.sread(w, a[0]) > x
+            return
         elif op == 's_cmp_lg_u32':
             w.scc = self.sread(w, a[0]) != x
             return
