@@ -264,8 +264,7 @@ def test_asm_forward_prescaled_in_simulator(lens_q, lens_k, H, D, grid, dtype, c
 def _run_text(txt, lens_q, lens_k, H, D, dtype, mode="lazy"):
     """_run with a given kernel text (the product kernel cache bypassed)."""
     saved = dict(_TXT)
-    if hd is None:
-        hd = 128 if D > 96 else 96 if D > 64 else 64 if D > 32 else 32
+    hd = 128 if D > 96 else 96 if D > 64 else 64 if D > 32 else 32
     _TXT.clear()
     _TXT[(dtype, hd, 4, False, gen_fwd.product_prescale(dtype, hd, 4, False))] = txt
     orig = asm_sim.Sim.__init__
