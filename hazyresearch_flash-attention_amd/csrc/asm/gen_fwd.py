@@ -1787,7 +1787,9 @@ def prologue_persist(g):
     def start_with_wait(n):
         st = [copy.copy(x) for x in sc['start']]
         i = next(k for k, x in enumerate(st) if x.txt.startswith('s_waitcnt vmcnt('))
-        st[i] = raw(f's_waitcnt vmcnt({n})')
+        # 'nostartwait' timing probe: no wait for the block's first K/V tiles (wrong results, the
+        # price of their latency at the block start)
+        st[i] = raw(f's_waitcnt vmcnt({63 if "nostartwait" in PROBE else n})')
         return st
     # the first wait waits for Q, K0, K1, V0: younger are K2 V1 K3 V2 (8 pieces) and the next Q's loads
     qs = ([S('s_cmp_lg_u32 s101, 0'), raw('s_cbranch_scc1 .Lqsdone')] + sc['qscale'] + [label('.Lqsdone')]
