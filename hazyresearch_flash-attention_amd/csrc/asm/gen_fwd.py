@@ -1685,7 +1685,7 @@ def set_prescale(on):
     """PRESCALE on/off (D = 64, 4 waves): the seed registers raise the VGPR count."""
     global PRESCALE, NVGPR
     if on:
-        assert D == 64 and NWAVES == 4 and ORDET
+        assert D in (32, 64) and NWAVES == 4 and ORDET
         NVGPR = max(NVGPR, V_SEED['B'] + 16)
     PRESCALE = on
 
@@ -2341,7 +2341,7 @@ def main():
         NVGPR = max(NVGPR, V_MCB['B'] + 4)
     global KARG_BYTES
     if 'pstamps' in PROBE:
-        assert args.hd == 64 and PERSIST and NVGPR <= PS_V
+        assert args.hd in (32, 64) and PERSIST and NVGPR <= PS_V
         NVGPR = 256
         KARG_BYTES += 8
     if 'stamps' in PROBE:

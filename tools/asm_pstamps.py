@@ -39,13 +39,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="8,12,2048")
     ap.add_argument("--gen", default="")
+    ap.add_argument("--hd", type=int, default=64, help="head-dim tile (64, or 32: head_dim 32)")
     args = ap.parse_args()
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)
-    img = build(out_dir, args.gen)
+    img = build(out_dir, args.gen + (f" --hd {args.hd}" if args.hd != 64 else ""))
     import torch
     B, H, S = (int(x) for x in args.shape.split(","))
-    D = 64
+    D = args.hd
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     q, k, v = (torch.randn(B * S, H, D, generator=g).bfloat16().to(dev) for _ in range(3))
@@ -73,7 +74,7 @@ def main():
     mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
     buf = ctypes.create_string_buffer(img, len(img))
     assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
-    assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"fa_fwd_d64p_bf16_asm") == 0
+    assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, f"fa_fwd_d{args.hd}p_bf16_asm".encode()) == 0
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for _ in range(300):     # clock ramp
         assert hip.hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, stream, None, extra) == 0
