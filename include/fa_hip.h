@@ -22,8 +22,9 @@
  *                              backward (flash_attn/rotary.py:22-41, 86-135)
  *   (fa_fwd runs hand-scheduled gfx950 assembly kernels, csrc/asm/gen_fwd.py, embedded in the library
  *    as code objects, for head_dim in (32, 64], 80, 96 or 128, fp16/bf16, causal or not, no dropout, dense,
- *    no fused rotary; the persistent form for
- *    non-causal grids with more blocks than CUs (fa_asm.cpp fwd_asm_eligible / persistent_grid_for).
+ *    no fused rotary; the persistent form for non-causal grids with more blocks than CUs, and at
+ *    head_dim <= 64 for every non-causal call with >= 1024 keys (its scores carry the rounding of
+ *    Q*softmax_scale*log2(e) to the input type; fa_asm.cpp fwd_asm_eligible / persistent_grid_for).
  *    FaFwdArgs.impl selects a form or the HIP kernels.)
  *   fa_query, fa_last_error, fa_version, fa_fwd_kernel_name: host helpers (no reference counterpart; the reference
  *                                                  raised through TORCH_CHECK / exit(1),
@@ -108,8 +109,8 @@ typedef struct FaFwdArgs {
     int64_t rot_stride;
     /* Kernel family (FA_IMPL_*). FA_IMPL_AUTO picks the fastest kernel for the shape: the
      * hand-scheduled assembly forward for head_dim in (32, 64], 80, 96 or 128, fp16/bf16, no dropout,
-     * dense, no fused rotary (non-causal grids with more blocks than CUs take
-     * its persistent form); the HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels;
+     * dense, no fused rotary (non-causal grids with more blocks than CUs, and head_dim <= 64 calls
+     * with >= 1024 keys, take its persistent form); the HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels;
      * FA_IMPL_ASM4 / FA_IMPL_ASM8 / FA_IMPL_ASM4P force the one-wave-per-SIMD, the
      * two-waves-per-SIMD and the persistent one-wave-per-SIMD assembly form where the shape is
      * eligible (tests compare them; results agree within fp32 rounding of the row sums). */
