@@ -76,11 +76,13 @@ def test_asm_forms_agree_at_north_star_grid():
         assert (o[:S, :2].float() - ref).abs().max().item() <= 1e-2, form
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("seqlen_k", [1, 17, 300])
 @pytest.mark.parametrize("amp", [1.0, 2.5])
-def test_asm_prescaled_score_rounding_bound(seqlen_k, amp):
+def test_asm_prescaled_score_rounding_bound(seqlen_k, amp, dtype):
     """The persistent D=64 bf16 form scores with Q c rounded to bf16 (c = softmax_scale log2 e,
-    gen_fwd PRESCALE): per score |error| <= 2^-9 softmax_scale sum_d |q_d k_d| (natural units). Short
+    gen_fwd PRESCALE; fp16: rounded to fp16, 2^-11): per score |error| <= 2^-9 softmax_scale sum_d |q_d k_d|
+    (natural units). Short
     key sets (one key: the LSE is that one score) and amplified inputs: the output keeps the 2x rule
     and the LSE stays within that bound plus tests/test_flash_attn.py's LSE tolerance."""
     import math
@@ -88,11 +90,12 @@ def test_asm_prescaled_score_rounding_bound(seqlen_k, amp):
     hip = _hip()
     B, H, Sq, d = 3, 4, 300, 64
     g = torch.Generator().manual_seed(seqlen_k)
-    q, k, v = ((torch.randn(B * n, H, d, generator=g) * s).bfloat16().to(DEV)
+    q, k, v = ((torch.randn(B * n, H, d, generator=g) * s).to(dtype).to(DEV)
                for n, s in ((Sq, amp), (seqlen_k, amp), (seqlen_k, 1.0)))
     cu_q = torch.arange(0, (B + 1) * Sq, Sq, dtype=torch.int32, device=DEV)
     cu_k = torch.arange(0, (B + 1) * seqlen_k, seqlen_k, dtype=torch.int32, device=DEV)
-    assert hip.fwd_kernel_name(B, H, d, Sq, seqlen_k, torch.bfloat16, impl=hip.FA_IMPL_ASM4P) == "fa_fwd_d64p_bf16_asm"
+    tag = "bf16" if dtype == torch.bfloat16 else "f16"
+    assert hip.fwd_kernel_name(B, H, d, Sq, seqlen_k, dtype, impl=hip.FA_IMPL_ASM4P) == f"fa_fwd_d64p_{tag}_asm"
     with hip.force_impl(hip.FA_IMPL_ASM4P):
         out, lse, _ = fi.flash_attn_unpadded_func(q, k, v, cu_q, cu_k, Sq, seqlen_k, 0.0, return_attn_probs=True)
     qb, kb, vb = (x.view(B, -1, H, d) for x in (q, k, v))
@@ -103,7 +106,8 @@ def test_asm_prescaled_score_rounding_bound(seqlen_k, amp):
     scale = d ** -0.5
     s = torch.einsum("bthd,bshd->bhts", qb.float(), kb.float()) * scale
     lse_ref = torch.logsumexp(s, -1)
-    rnd = 2 ** -9 * scale * torch.einsum("bthd,bshd->bhts", qb.float().abs(), kb.float().abs()).amax(-1)
+    u = 2 ** -9 if dtype == torch.bfloat16 else 2 ** -11
+    rnd = u * scale * torch.einsum("bthd,bshd->bhts", qb.float().abs(), kb.float().abs()).amax(-1)
     dev = (lse[:, :, :Sq] - lse_ref).abs()
     bound = 2e-3 + 1e-3 * lse_ref.abs() + rnd
     assert (dev <= bound).all(), (dev.max().item(), (dev - bound).max().item())
