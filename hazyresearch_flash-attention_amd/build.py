@@ -111,6 +111,7 @@ def build_asm(force=False):
         form = ["--persist", "1"] if nw == "p" else ["--waves", str(nw)]
         # FA_ASM_GEN_FLAGS: extra generator switches for a variant library (A/B tools only)
         extra = os.environ.get("FA_ASM_GEN_FLAGS", "").split()
+        extra += os.environ.get(f"FA_ASM_GEN_FLAGS_D{hd}", "").split()     # one tile only
         _run([sys.executable, ASM_GEN, "--dtype", dt, "--hd", str(hd)] + form + extra + ["--out", asm])
         _run([os.path.join(LLVM_BIN, "clang"), "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
               f"-mcpu={ARCH}", "-c", asm, "-o", obj])
