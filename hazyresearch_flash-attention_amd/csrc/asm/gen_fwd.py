@@ -1691,10 +1691,11 @@ def set_prescale(on):
 
 
 def product_prescale(dtype, hd, waves, persist):
-    """The shipped setting (build.py, tests): PRESCALE for the D = 64 persistent form only. Its
-    scores carry the rounding of Q c to the input type (|error| <= 2^-9 c sum_d |q_d k_d|); the
-    one-block forms (causal, small grids, FA_IMPL_ASM4) keep fp32-exact scores."""
-    return hd == 64 and waves == 4 and persist and PRESCALE_PRODUCT.get(dtype, False)
+    """The shipped setting (build.py, tests): PRESCALE for the D = 64 persistent form, and at fp16
+    for the one-block form too. Its scores carry the rounding of Q c to the input type (|error| <=
+    2^-9 c sum_d |q_d k_d| for bf16, 2^-11 for fp16); the bf16 one-block forms (causal, small grids,
+    FA_IMPL_ASM4) keep fp32-exact scores."""
+    return hd == 64 and waves == 4 and (persist or dtype == 'f16') and PRESCALE_PRODUCT.get(dtype, False)
 
 
 PRESCALE_PRODUCT = {'bf16': True, 'f16': True}
