@@ -207,7 +207,7 @@ static int persist_grid() {
 // than CUs (measured -1.8 % at the north star's 3 rounds, -3.4 % at 6; D=128 -1.6 % at 3 rounds,
 // even at 12), and at D=64 with 1024+ keys at any grid size (its pre-scaled Q, gen_fwd.py
 // PRESCALE, is the persistent form's only: C5, 256 blocks on 256 CUs, 64.2 vs 69.8 us; C2's 8-tile
-// blocks lose, 14.4 vs 14.0 us, tools/r04_forms.sh; shorter key sets keep fp32-exact scores);
+// blocks lose, 14.4 vs 14.0 us, tools/r04_forms.sh; at bf16 the one-block form keeps fp32-exact scores);
 // FA_IMPL_ASM4P forces it. Causal grids keep the dispatcher's dynamic balance.
 static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
     if (a.is_causal || a.impl == FA_IMPL_ASM4 || a.impl == FA_IMPL_ASM8) return 0;
