@@ -149,11 +149,12 @@ def rqn(base, n=4):
 
 
 # LDS ring per form: (slots, DMA distance, one barrier per two tiles, persistent K/V tail). D <= 64
-# (4 waves): 6 slots (96 KiB), distance 4, a barrier after odd tiles only (a fast wave leads by up
-# to two tiles, so a slot is rewritten two tiles after its last read) and no K/V tail (its seam
+# (4 waves): 6 slots (96 KiB), distance 3, a barrier after odd tiles only (a fast wave leads by up
+# to two tiles, so a slot is rewritten two tiles after its last read; distance 3 also lets the
+# prologue skip its barrier after the K0 reads) and no K/V tail (its seam
 # saving measured ~0 once tile 0 stopped taking the rescale; the tail needs nt % R == 0). D = 128
 # (32 KiB per slot) and the 8-wave form keep 4 slots, distance 3, a barrier per tile.
-GEOMETRY = {(64, 4): (6, 4, True, False), (32, 4): (6, 4, True, False),
+GEOMETRY = {(64, 4): (6, 3, True, False), (32, 4): (6, 3, True, False),
             (128, 4): (4, 3, False, True), (96, 4): (4, 3, False, True), (64, 8): (4, 3, False, True)}
 D_NAME = 64            # the tile named in the kernel symbol (96: the D = 128 layout computing 96 columns)
 
@@ -1582,8 +1583,11 @@ def prologue_sections(g):
     p += [raw('s_barrier')]
     p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
     p += pstamp(PS_V + 4)
-    # every wave reads K0 before any wave passes the next barrier: tile 0 DMAs K4 into K0's slot
-    p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)'), raw('s_barrier')] + g.qk('A', 0)
+    # every wave reads K0 before any wave passes the next barrier when the loop's first DMA into K0's
+    # slot (tile R - 1 - DIST) comes before its first barrier (after tile 0, or tile 1 with BAR2):
+    # R 4 / DIST 3 (tile 0 DMAs K4 into slot 0) needs this one, R 6 / DIST 3 with BAR2 does not
+    kbar = [raw('s_barrier')] if R - 1 - DIST < (2 if BAR2 else 1) or NWAVES == 8 else []
+    p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)')] + kbar + g.qk('A', 0)
     if FIRST_MAX and NWAVES == 4 and ORDET:
         p += g.first_max()
     if NWAVES == 8:
