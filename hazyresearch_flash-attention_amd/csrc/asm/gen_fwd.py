@@ -75,7 +75,7 @@ KSPLIT_LAG = 3         # ... each at least this many MFMAs ahead of its QK MFMA
 KSPLIT = 3             # K(t+1) fragment reads moved from phase 1 to the start of phase 2 (D = 64)
 FIRST_MAX = True       # prologue: tile 0's row max sets the starting shift (no rescale at tile 0)
 LAST_UNMASKED = True   # last tile: unmasked copy when every row sees the whole tile
-MFMA_ZERO = True       # prologue: O, row sums, V buffer zeroed by MFMAs of a zero operand (D <= 64)
+MFMA_ZERO = True       # prologue: O, row sums, V buffer zeroed by MFMAs of a zero operand
 ORDET_ANDOR = True     # ORDET: the last P word enters the test by one v_and_or_b32 (mask in V_MTHR)
 PHASE_TAIL = 1         # ORDET test issued before the phase's last PHASE_TAIL MFMAs, its branch after them
 
@@ -1537,13 +1537,13 @@ def prologue_sections(g):
     p.append(sec('qscale'))
     p += q_prescale(g)
     p.append(sec('zero'))
-    if QL_VGPR:
-        p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(D)]
+    if QL_VGPR:     # row sums in VGPRs (D = 128 layout)
         p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(A_L['A'], A_L['B'] + 4)]
     vf1 = A_VF + KFB * ((-1) % NBV)
-    if QL_VGPR or not MFMA_ZERO:
-        if not QL_VGPR:
-            p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(A_ONES)]
+    # O (and, below D = 128, the row sums) in AGPRs from a0
+    o_regs = D if QL_VGPR else A_ONES
+    if not MFMA_ZERO:
+        p += [Inst(f'v_accvgpr_write_b32 a{r}, v32', 'accw', rd=['v32'], wr=[f'a{r}']) for r in range(o_regs)]
         p += [Inst(f'v_accvgpr_write_b32 a{vf1 + r}, v32', 'accw', rd=['v32'], wr=[f'a{vf1 + r}'])
               for r in range(KFB)]
         p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
@@ -1552,7 +1552,7 @@ def prologue_sections(g):
         # products of that zero with C = 0 (16 / 4 AGPRs per instruction instead of one)
         p += [V(f'v_mov_b32 v{r}, 0', r, []) for r in range(V_P['B'], V_P['B'] + 16)]
         z = V_P['B']
-        for lo, n in ((0, A_ONES), (vf1, KFB)):
+        for lo, n in ((0, o_regs), (vf1, KFB)):
             r = lo
             while r < lo + n:
                 if lo + n - r >= 16 and r % 16 == 0:
