@@ -1695,14 +1695,16 @@ def set_prescale(on):
 
 
 def product_prescale(dtype, hd, waves, persist):
-    """The shipped setting (build.py, tests): PRESCALE for the D = 64 persistent form, and at fp16
-    for the one-block form too. Its scores carry the rounding of Q c to the input type (|error| <=
-    2^-9 c sum_d |q_d k_d| for bf16, 2^-11 for fp16); the bf16 one-block forms (causal, small grids,
-    FA_IMPL_ASM4) keep fp32-exact scores."""
+    """The shipped setting (build.py, tests): no form is pre-scaled since round 5. PRESCALE scores
+    carry the rounding of Q c to the input type (|error| <= 2^-9 c sum_d |q_d k_d| for bf16, 2^-11
+    for fp16); on a ragged batch with 1..5-key sequences and at softmax_scale 1.0 it broke the LSE
+    tolerance (up to 16x) and the reference's 2x rule on dV (1.5x bf16, 1.75x fp16) where the
+    fp32-exact forms pass (tools/r05/prescale_diag.py). It stays a generator switch
+    (--prescale 1) for A/B only."""
     return hd == 64 and waves == 4 and (persist or dtype == 'f16') and PRESCALE_PRODUCT.get(dtype, False)
 
 
-PRESCALE_PRODUCT = {'bf16': True, 'f16': True}
+PRESCALE_PRODUCT = {'bf16': False, 'f16': False}
 
 
 def set_persist(on):

@@ -76,11 +76,17 @@ const char *fa_last_error(void) { return g_last_error.c_str(); }
 const char *fa_version(void) { return "fa_hip 0.1.0 (gfx950)"; }
 
 const char *fa_fwd_kernel_name(const FaFwdArgs *a) {
-    if (a == nullptr || a->head_dim <= 0 || a->head_dim > 128 || a->batch <= 0 || a->nheads <= 0) return nullptr;
+    // the checks fwd_impl makes before it launches anything (NULL: fa_fwd would fail or launch nothing)
+    if (a == nullptr || a->head_dim <= 0 || a->head_dim > 128 || a->head_dim % 8 != 0 || a->batch <= 0 ||
+        a->nheads <= 0 || a->max_seqlen_q <= 0 || a->max_seqlen_k < 0 ||
+        (a->dtype != FA_DTYPE_FP16 && a->dtype != FA_DTYPE_BF16) || a->impl < FA_IMPL_AUTO || a->impl > FA_IMPL_ASM4P ||
+        a->p_dropout < 0.f || a->p_dropout >= 1.f)
+        return nullptr;
     if (fa::fwd_asm_eligible(*a, FaBlockMask{nullptr, 0, 0, 0})) return fa::asm_kernel_name(*a);
-    const int t = a->head_dim <= 32 ? 32 : a->head_dim <= 64 ? 64 : 128;
-    return t == 32 ? "fa_fwd_kernel (HIP, D=32 tile)" : t == 64 ? "fa_fwd_kernel (HIP, D=64 tile)"
-                                                          : "fa_fwd_kernel (HIP, D=128 tile)";
+    // HIP family: the prefix of the demangled template name a rocprofv3 trace shows
+    // ("void fa::fa_fwd_kernel<64, fa::Bf16, ...>(FaFwdArgs, FaBlockMask, int)")
+    const int t = pick_tile(a->head_dim);
+    return t == 32 ? "fa::fa_fwd_kernel<32," : t == 64 ? "fa::fa_fwd_kernel<64," : "fa::fa_fwd_kernel<128,";
 }
 
 int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {

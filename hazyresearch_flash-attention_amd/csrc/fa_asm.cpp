@@ -5,9 +5,9 @@
 // loaded per device on first use with hipModuleLoadData and launched with hipModuleLaunchKernel
 // on the caller's stream (so it is captured into hipGraphs like the HIP kernels).
 //
-// It serves the north-star shape class: head_dim in (32, 64] (the D=64 tile) or 128 (the D=128
-// tile), fp16/bf16, causal or not, no dropout, dense (no block mask), no fused rotary. Everything else keeps the HIP
-// kernels of fa_fwd_kernel.h. Semantics are the same: var-len sequences through cu_seqlens,
+// It serves head_dim in (32, 64] (the D=64 tile), 80 and 96 (the D=96 tile: the D=128 layout computing
+// 96 columns) and 128 (the D=128 tile), fp16/bf16, causal or not, no dropout, dense (no block mask), no
+// fused rotary. Everything else keeps the HIP kernels of fa_fwd_kernel.h. Semantics are the same: var-len sequences through cu_seqlens,
 // rows past a sequence neither read nor written, LSE = m*scale + ln(sum) (-inf for no keys).
 #include <hip/hip_runtime.h>
 
@@ -106,7 +106,9 @@ DevFns g_fns[kMaxDev];
 // loads run with this thread's capture mode exchanged to relaxed (module loading is not a stream
 // operation; in global mode the runtime may refuse it), and if they still fail the caller falls back
 // to the HIP kernels (fa_api.cpp) instead of failing the capture.
-hipError_t load_all(DevFns &d) {
+// Each module loads on its own (one that fails does not stop the others); the call reports the status
+// of the requested form `want` only.
+hipError_t load_all(DevFns &d, int want) {
     static const void *const imgs[kNumFns] = {fa_asm_fwd_d64_bf16,   fa_asm_fwd_d64_f16,
                                               fa_asm_fwd_d128_bf16,  fa_asm_fwd_d128_f16,
                                               fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16,
@@ -123,15 +125,27 @@ hipError_t load_all(DevFns &d) {
                                                "fa_fwd_d96p_bf16_asm",  "fa_fwd_d96p_f16_asm"};
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     const bool exchanged = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
-    hipError_t e = hipSuccess;
-    for (int k = 0; k < kNumFns && e == hipSuccess; ++k) {
-        if (d.fn[k]) continue;
-        e = hipModuleLoadData(&d.mod[k], imgs[k]);
-        if (e == hipSuccess) e = hipModuleGetFunction(&d.fn[k], d.mod[k], names[k]);
-        if (e != hipSuccess) d.fn[k] = nullptr;
+    hipError_t want_e = hipErrorNotFound;
+    for (int k = 0; k < kNumFns; ++k) {
+        if (d.fn[k]) {
+            if (k == want) want_e = hipSuccess;
+            continue;
+        }
+        hipModule_t m = nullptr;
+        hipError_t e = hipModuleLoadData(&m, imgs[k]);
+        if (e == hipSuccess) {
+            e = hipModuleGetFunction(&d.fn[k], m, names[k]);
+            if (e == hipSuccess) {
+                d.mod[k] = m;
+            } else {
+                d.fn[k] = nullptr;
+                (void)hipModuleUnload(m);
+            }
+        }
+        if (k == want) want_e = e;
     }
     if (exchanged) hipThreadExchangeStreamCaptureMode(&mode);
-    return e;
+    return want_e;
 }
 
 hipError_t get_function(int dtype, int form, hipFunction_t *out) {
@@ -143,7 +157,7 @@ hipError_t get_function(int dtype, int form, hipFunction_t *out) {
     std::lock_guard<std::mutex> lk(g_mu);
     DevFns &d = g_fns[dev];
     if (!d.fn[k]) {
-        e = load_all(d);
+        e = load_all(d, k);
         if (e != hipSuccess || !d.fn[k]) return e != hipSuccess ? e : hipErrorNotFound;
     }
     *out = d.fn[k];
@@ -203,18 +217,16 @@ static int persist_grid() {
     return g;
 }
 
-// The persistent form (D=64 and D=128 tiles, non-causal): by default when the grid has more blocks
-// than CUs (measured -1.8 % at the north star's 3 rounds, -3.4 % at 6; D=128 -1.6 % at 3 rounds,
-// even at 12), and at D=64 with 1024+ keys at any grid size (its pre-scaled Q, gen_fwd.py
-// PRESCALE, is the persistent form's only: C5, 256 blocks on 256 CUs, 64.2 vs 69.8 us; C2's 8-tile
-// blocks lose, 14.4 vs 14.0 us, tools/r04_forms.sh; at bf16 the one-block form keeps fp32-exact scores);
-// FA_IMPL_ASM4P forces it. Causal grids keep the dispatcher's dynamic balance.
+// The persistent form (D=64, D=96 and D=128 tiles, non-causal): by default when the grid has more
+// blocks than CUs (measured -1.8 % at the north star's 3 rounds, -3.4 % at 6; D=128 -1.6 % at 3
+// rounds, even at 12); FA_IMPL_ASM4P forces it. Causal grids keep the dispatcher's dynamic balance.
+// Every form computes fp32-exact scores (round 5: the pre-scaled Q of round 4, gen_fwd.py PRESCALE,
+// is out of the product), so the choice is by grid shape only, never by key count.
 static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
     if (a.is_causal || a.impl == FA_IMPL_ASM4 || a.impl == FA_IMPL_ASM8) return 0;
     const int g = persist_grid();
     if (g < 8) return 0;
-    const bool prescaled = a.head_dim <= 64 && a.max_seqlen_k >= 1024;
-    if (a.impl == FA_IMPL_ASM4P || prescaled) return (int)(nwg < (uint32_t)g ? nwg : (uint32_t)g);
+    if (a.impl == FA_IMPL_ASM4P) return (int)(nwg < (uint32_t)g ? nwg : (uint32_t)g);
     return nwg > (uint32_t)g ? g : 0;
 }
 

@@ -17,6 +17,7 @@
 #include <torch/csrc/utils/pybind.h>
 
 #include <cmath>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -414,6 +415,28 @@ void rotary_call(const at::Tensor &x, const at::Tensor &y, const at::Tensor &cos
     if (rc != 0) raise_rc(rc, "fa_rotary");
 }
 
+// True when fa_fwd takes an assembly kernel for the unrotated dense call of this shape
+// (include/fa_hip.h fa_fwd_kernel_name).
+bool asm_forward_for(int64_t B, int64_t S, int64_t H, int64_t D, double p, bool causal, double scale,
+                     at::ScalarType t) {
+    FaFwdArgs a{};
+    a.q_row_stride = a.k_row_stride = a.v_row_stride = 3 * H * D;
+    a.o_row_stride = H * D;
+    a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = D;
+    a.batch = (int32_t)B;
+    a.nheads = (int32_t)H;
+    a.head_dim = (int32_t)D;
+    a.max_seqlen_q = a.max_seqlen_k = (int32_t)S;
+    a.lse_stride = (int32_t)std::max<int64_t>(round16(S), 16);
+    a.softmax_scale = (float)scale;
+    a.p_dropout = (float)p;
+    a.is_causal = causal ? 1 : 0;
+    a.dtype = dtype_code(t);
+    a.impl = FA_IMPL_AUTO;
+    const char *name = fa_fwd_kernel_name(&a);
+    return name != nullptr && std::strstr(name, "_asm") != nullptr;
+}
+
 // FlashAttnRotaryQKVFunc (flash_attention.py): padded contiguous qkv (B, S, 3, H, D); k rotated by
 // one fa_rotary pass, q rotated inside the forward at its load; backward rotates q once more, runs
 // the attention backward on (q_rot, k_rot, v) and rotates dq, dk back in place.
@@ -425,10 +448,24 @@ struct FlashAttnRotaryQKVFn : public torch::autograd::Function<FlashAttnRotaryQK
         const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
         c10::DeviceGuard guard(qkv.device());
         at::Tensor cos = cos_in.slice(0, 0, S).contiguous(), sin = sin_in.slice(0, 0, S).contiguous();
+        at::Tensor flat = qkv.view({B * S, 3, H, D});
+        if (asm_forward_for(B, S, H, D, p, causal, scale, qkv.scalar_type())) {
+            // the Q rotation at the kernel's Q load exists in the HIP forward only: where fa_fwd takes an
+            // assembly kernel, one fa_rotary pass rotates q and k into (B, S, 2, H, D) and the assembly
+            // forward reads them (the backward reuses both rotated tensors: no second q pass)
+            at::Tensor qk_rot = at::empty({B, S, 2, H, D}, qkv.options());
+            rotary_call(qkv, qk_rot, cos, sin, {B, S, 2, H, D}, {S * 3 * H * D, 3 * H * D, H * D, D},
+                        {S * 2 * H * D, 2 * H * D, H * D, D}, 2, false);
+            at::Tensor qk = qk_rot.view({B * S, 2, H, D});
+            auto r = fwd(qk.select(1, 0), qk.select(1, 1), flat.select(1, 2), cu, cu, S, S, p, scale, false, causal,
+                         false, seed, offset, od_ptr(od), FA_IMPL_AUTO);
+            ctx->save_for_backward({qkv, qk_rot, r[0], r[1], cos, sin, cu});
+            save_cfg(ctx, S, S, p, scale, causal, seed, offset, od);
+            return {r[0].view({B, S, H, D})};
+        }
         at::Tensor k_rot = at::empty({B, S, H, D}, qkv.options());
         rotary_call(qkv.select(2, 1), k_rot, cos, sin, {B, S, 1, H, D}, {S * 3 * H * D, 3 * H * D, 0, D},
                     {S * H * D, H * D, 0, D}, 1, false);
-        at::Tensor flat = qkv.view({B * S, 3, H, D});
         auto r = fwd(flat.select(1, 0), k_rot.view({B * S, H, D}), flat.select(1, 2), cu, cu, S, S, p, scale, false,
                      causal, false, seed, offset, od_ptr(od), FA_IMPL_AUTO, cos, sin);
         ctx->save_for_backward({qkv, k_rot, r[0], r[1], cos, sin, cu});
@@ -441,12 +478,21 @@ struct FlashAttnRotaryQKVFn : public torch::autograd::Function<FlashAttnRotaryQK
         const at::Tensor &qkv = t[0], &k_rot = t[1], &out = t[2], &lse = t[3], &cos = t[4], &sin = t[5], &cu = t[6];
         const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
         c10::DeviceGuard guard(qkv.device());
-        at::Tensor q_rot = at::empty({B, S, H, D}, qkv.options());
-        rotary_call(qkv.select(2, 0), q_rot, cos, sin, {B, S, 1, H, D}, {S * 3 * H * D, 3 * H * D, 0, D},
-                    {S * H * D, H * D, 0, D}, 1, false);
+        at::Tensor q_rot, kr;
+        if (k_rot.dim() == 5) {     // (B, S, 2, H, D): q and k rotated by the forward (assembly forward)
+            at::Tensor qk = k_rot.view({B * S, 2, H, D});
+            q_rot = qk.select(1, 0);
+            kr = qk.select(1, 1);
+        } else {
+            q_rot = at::empty({B, S, H, D}, qkv.options());
+            rotary_call(qkv.select(2, 0), q_rot, cos, sin, {B, S, 1, H, D}, {S * 3 * H * D, 3 * H * D, 0, D},
+                        {S * H * D, H * D, 0, D}, 1, false);
+            q_rot = q_rot.view({B * S, H, D});
+            kr = k_rot.view({B * S, H, D});
+        }
         at::Tensor dqkv = at::empty_like(qkv);
         at::Tensor d = dqkv.view({B * S, 3, H, D});
-        bwd(g[0].reshape({B * S, H, D}), q_rot.view({B * S, H, D}), k_rot.view({B * S, H, D}),
+        bwd(g[0].reshape({B * S, H, D}), q_rot, kr,
             qkv.view({B * S, 3, H, D}).select(1, 2), out, lse, d.select(1, 0), d.select(1, 1), d.select(1, 2), cu, cu,
             S, S, s.p, s.scale, false, s.causal, s.seed, s.offset, od_ptr(s.od));
         const std::array<int64_t, 4> st3{S * 3 * H * D, 3 * H * D, H * D, D};

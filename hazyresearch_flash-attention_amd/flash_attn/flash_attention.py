@@ -75,9 +75,12 @@ class FlashAttnRotaryQKVFunc:
 class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
     """Attention over a padded, contiguous qkv (B, S, 3, H, D) with rotary embeddings fused into
     the forward (README.md:56 "Fuse rotary embedding"; rotation = rotary.py:31-41):
-    * forward: k is rotated by one fa_rotary pass into a (B, S, H, D) buffer (the backward needs it
-      anyway); q is rotated by fa_fwd at its one-time fragment load, never written to HBM. The
-      operands are bit-identical to rotating q and k first (same rounding, fa_common.h rotary8).
+    * forward: where fa_fwd takes an assembly kernel (no dropout, head_dim in (32, 64], 80, 96, 128)
+      one fa_rotary pass rotates q and k into a (B, S, 2, H, D) buffer and the assembly forward reads
+      it (measured faster than the HIP forward rotating q at its load); otherwise k
+      is rotated by one fa_rotary pass into a (B, S, H, D) buffer (the backward needs it anyway) and
+      q by the HIP fa_fwd at its one-time fragment load, never written to HBM. The operands are
+      bit-identical to rotating q and k first (same rounding, fa_common.h rotary8).
     * backward: q is rotated once more (fa_rotary), the attention backward runs on (q_rot, k_rot,
       v), and dq, dk are rotated back in place (the autograd transpose, fa_rotary inverse)."""
 
@@ -88,16 +91,29 @@ class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
         B, S, _, H, D = qkv.shape
         assert qkv.is_contiguous()
         cos, sin = cos[:S].contiguous(), sin[:S].contiguous()
-        st = (S * 3 * H * D, 3 * H * D, 0, D)
-        k_rot = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
-        hip.rotary(qkv[:, :, 1], k_rot, cos, sin, (B, S, 1, H, D), st, (S * H * D, H * D, 0, D), 1, False)
         if softmax_scale is None:
             softmax_scale = D ** (-0.5)
         rng_state = _reserve(dropout_p, qkv.device)
         flat = qkv.view(B * S, 3, H, D)
         cu = _uniform_cu_seqlens(B, S, qkv.device)
-        out, lse = hip.fwd(flat[:, 0], k_rot.view(B * S, H, D), flat[:, 2], cu, cu, S, S, dropout_p, softmax_scale,
-                           False, causal, False, None, rng_state=rng_state, rotary=(cos, sin))
+        name = hip.fwd_kernel_name(B, H, D, S, S, qkv.dtype, causal, dropout_p, row_elems=3 * H * D)
+        if name is not None and name.endswith("_asm"):
+            # the Q rotation at the Q load exists in the HIP forward only: where fa_fwd takes an
+            # assembly kernel, one fa_rotary pass rotates q and k (B, S, 2, H, D) and the assembly
+            # forward reads them (the backward reuses both: no second q pass)
+            qk_rot = torch.empty((B, S, 2, H, D), dtype=qkv.dtype, device=qkv.device)
+            hip.rotary(qkv, qk_rot, cos, sin, (B, S, 2, H, D), (S * 3 * H * D, 3 * H * D, H * D, D),
+                       (S * 2 * H * D, 2 * H * D, H * D, D), 2, False)
+            qk = qk_rot.view(B * S, 2, H, D)
+            out, lse = hip.fwd(qk[:, 0], qk[:, 1], flat[:, 2], cu, cu, S, S, dropout_p, softmax_scale,
+                               False, causal, False, None, rng_state=rng_state)
+            k_rot = qk_rot
+        else:
+            st = (S * 3 * H * D, 3 * H * D, 0, D)
+            k_rot = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
+            hip.rotary(qkv[:, :, 1], k_rot, cos, sin, (B, S, 1, H, D), st, (S * H * D, H * D, 0, D), 1, False)
+            out, lse = hip.fwd(flat[:, 0], k_rot.view(B * S, H, D), flat[:, 2], cu, cu, S, S, dropout_p,
+                               softmax_scale, False, causal, False, None, rng_state=rng_state, rotary=(cos, sin))
         ctx.save_for_backward(qkv, k_rot, out, lse, cos, sin, cu)
         ctx.rng_state, ctx.dropout_p, ctx.softmax_scale, ctx.causal = rng_state, dropout_p, softmax_scale, causal
         return out.view(B, S, H, D)
@@ -107,12 +123,17 @@ class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
         from flash_attn import flash_attn_hip as hip
         qkv, k_rot, out, lse, cos, sin, cu = ctx.saved_tensors
         B, S, _, H, D = qkv.shape
-        st = (S * 3 * H * D, 3 * H * D, 0, D)
-        q_rot = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
-        hip.rotary(qkv[:, :, 0], q_rot, cos, sin, (B, S, 1, H, D), st, (S * H * D, H * D, 0, D), 1, False)
+        if k_rot.dim() == 5:     # (B, S, 2, H, D): q and k rotated by the forward (assembly forward)
+            qk = k_rot.view(B * S, 2, H, D)
+            q_rot, k_rot = qk[:, 0], qk[:, 1]
+        else:
+            st = (S * 3 * H * D, 3 * H * D, 0, D)
+            q_rot = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
+            hip.rotary(qkv[:, :, 0], q_rot, cos, sin, (B, S, 1, H, D), st, (S * H * D, H * D, 0, D), 1, False)
+            q_rot, k_rot = q_rot.view(B * S, H, D), k_rot.view(B * S, H, D)
         dqkv = torch.empty_like(qkv)
         d = dqkv.view(B * S, 3, H, D)
-        hip.bwd(dout.reshape(B * S, H, D), q_rot.view(B * S, H, D), k_rot.view(B * S, H, D),
+        hip.bwd(dout.reshape(B * S, H, D), q_rot, k_rot,
                 qkv.view(B * S, 3, H, D)[:, 2], out, lse, d[:, 0], d[:, 1], d[:, 2], cu, cu, S, S, ctx.dropout_p,
                 ctx.softmax_scale, False, ctx.causal, None, rng_state=ctx.rng_state)
         st3 = (S * 3 * H * D, 3 * H * D, H * D, D)

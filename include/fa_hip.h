@@ -22,9 +22,8 @@
  *                              backward (flash_attn/rotary.py:22-41, 86-135)
  *   (fa_fwd runs hand-scheduled gfx950 assembly kernels, csrc/asm/gen_fwd.py, embedded in the library
  *    as code objects, for head_dim in (32, 64], 80, 96 or 128, fp16/bf16, causal or not, no dropout, dense,
- *    no fused rotary; the persistent form for non-causal grids with more blocks than CUs, and at
- *    head_dim <= 64 for every non-causal call with >= 1024 keys (its scores carry the rounding of
- *    Q*softmax_scale*log2(e) to the input type; fa_asm.cpp fwd_asm_eligible / persistent_grid_for).
+ *    no fused rotary; the persistent form for non-causal grids with more blocks than CUs; every form
+ *    computes fp32-exact scores; fa_asm.cpp fwd_asm_eligible / persistent_grid_for).
  *    FaFwdArgs.impl selects a form or the HIP kernels.)
  *   fa_query, fa_last_error, fa_version, fa_fwd_kernel_name: host helpers (no reference counterpart; the reference
  *                                                  raised through TORCH_CHECK / exit(1),
@@ -109,11 +108,12 @@ typedef struct FaFwdArgs {
     int64_t rot_stride;
     /* Kernel family (FA_IMPL_*). FA_IMPL_AUTO picks the fastest kernel for the shape: the
      * hand-scheduled assembly forward for head_dim in (32, 64], 80, 96 or 128, fp16/bf16, no dropout,
-     * dense, no fused rotary (non-causal grids with more blocks than CUs, and head_dim <= 64 calls
-     * with >= 1024 keys, take its persistent form); the HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels;
-     * FA_IMPL_ASM4 / FA_IMPL_ASM8 / FA_IMPL_ASM4P force the one-wave-per-SIMD, the
-     * two-waves-per-SIMD and the persistent one-wave-per-SIMD assembly form where the shape is
-     * eligible (tests compare them; results agree within fp32 rounding of the row sums). */
+     * dense, no fused rotary (non-causal grids with more blocks than CUs take its persistent form); the
+     * HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels; FA_IMPL_ASM4 / FA_IMPL_ASM8 /
+     * FA_IMPL_ASM4P force the one-wave-per-SIMD, the two-waves-per-SIMD and the persistent
+     * one-wave-per-SIMD assembly form where the shape is eligible. The three assembly forms compute the
+     * same fp32-exact scores and sums in the same order (bitwise equal outputs); the HIP kernels differ
+     * from them in the last bits (summation order), all within the reference's 2x rule. */
     int32_t impl;
     int32_t reserved;         /* 0 */
 } FaFwdArgs;
@@ -242,9 +242,12 @@ const char *fa_last_error(void);
 /* Library version string. */
 const char *fa_version(void);
 
-/* Name of the GPU kernel fa_fwd would launch for these arguments (e.g. "fa_fwd_d64p_bf16_asm"), as
- * it appears in a rocprofv3 kernel trace; NULL if the arguments are invalid. Launches nothing
- * (host helper, like fa_query; used by bench.py to name the kernel its roofline measures). */
+/* Name of the GPU kernel fa_fwd would launch for these arguments: an assembly kernel's symbol exactly
+ * as a rocprofv3 kernel trace shows it (e.g. "fa_fwd_d64p_bf16_asm"), or for the HIP template family
+ * the prefix of its demangled name in that trace ("fa::fa_fwd_kernel<64," of
+ * "void fa::fa_fwd_kernel<64, fa::Bf16, ...>(...)"). NULL when fa_fwd would reject the arguments or
+ * launch nothing (max_seqlen_q == 0). Launches nothing (host helper, like fa_query; used by bench.py
+ * to name the kernel its roofline measures). */
 const char *fa_fwd_kernel_name(const FaFwdArgs *args);
 
 #ifdef __cplusplus

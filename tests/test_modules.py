@@ -129,9 +129,10 @@ def test_flash_mha_module(rotary, padded, dtype):
 @pytest.mark.parametrize("D", [32, 64, 128])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_fused_rotary_equals_separate_pass(causal, D, dtype):
-    """Rotary fused into the forward's Q load (FlashAttnRotaryQKVFunc) gives the same output bits
-    as rotating q and k first (fa_rotary) and running the plain forward; its backward gives the
-    same dk/dv bits and dq up to the order of the fp32 dQ atomics (D <= 64)."""
+    """FlashAttnRotaryQKVFunc gives the same output bits as rotating q and k first (fa_rotary) and
+    running the plain forward, whichever route it takes: D = 32 rotates q inside the HIP forward at
+    its Q load, D = 64 / 128 (assembly forward) rotates q and k in one fa_rotary pass; its backward
+    gives the same dk/dv bits and dq up to the order of the fp32 dQ atomics (D <= 64)."""
     from flash_attn.flash_attention import FlashAttnRotaryQKVFunc
     from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func
     from flash_attn.rotary import apply_rotary_emb_qkv_
@@ -147,8 +148,9 @@ def test_fused_rotary_equals_separate_pass(causal, D, dtype):
     rot = apply_rotary_emb_qkv_(b.clone(), cos, sin)
     cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device="cuda")
     from flash_attn import flash_attn_hip as hip
-    with hip.force_impl(hip.FA_IMPL_HIP):   # the HIP kernels, as the fused-rotary forward uses
-        out_s = flash_attn_unpadded_qkvpacked_func(rot.reshape(B * S, 3, H, D), cu, S, 0.0, causal=causal)
+    name = hip.fwd_kernel_name(B, H, D, S, S, dtype, causal, row_elems=3 * H * D)
+    assert name.endswith("_asm") == (D != 32), name
+    out_s = flash_attn_unpadded_qkvpacked_func(rot.reshape(B * S, 3, H, D), cu, S, 0.0, causal=causal)
     assert torch.equal(out_f.reshape(B * S, H, D), out_s)
     ga, = torch.autograd.grad(out_f, a, dout)
     gb, = torch.autograd.grad(out_s, b, dout.reshape(B * S, H, D))
