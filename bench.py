@@ -128,18 +128,21 @@ def cpu_baseline(B, H, S, D):
 
 
 def read_traffic():
-    """HBM bytes per forward launch from the committed PMC summary (profiles/*_fwd_pmc.json), or None."""
+    """(HBM bytes per forward launch, source): from the newest committed PMC summary of this kernel
+    (profiles/<round>_fwd_pmc.json: FETCH_SIZE x 2 + WRITE_SIZE of separate rocprofv3 --pmc passes,
+    tools/round_end_profile.sh), not measured inside this run (PMC passes need their own profiled
+    processes); (None, None) if there is none."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
-        return None
+        return None, None
     cands = sorted(f for f in os.listdir(pdir) if f.endswith("_fwd_pmc.json"))
     if not cands:
-        return None
+        return None, None
     try:
         with open(os.path.join(pdir, cands[-1])) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            return json.load(f).get("hbm_bytes_per_launch"), "profiles/" + cands[-1]
     except Exception:
-        return None
+        return None, None
 
 
 def main():
@@ -206,8 +209,11 @@ def main():
     # kernel-level roofline: HIP events around each launch on the launch stream
     avg_ms, min_ms = time_events(step, max(args.steps, 20), 3)
     achieved = flops / (avg_ms * 1e-3) / 1e12
+    traffic, traffic_src = read_traffic()
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": read_traffic(),
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "traffic_source": f"{traffic_src} (committed PMC summary of this kernel, not this run)"
+                if traffic_src else None,
                 "measured_mfma_ceiling": MFMA_CEILING_RANDOM_TFLOPS,
                 "frac_of_measured_ceiling": round(achieved / MFMA_CEILING_RANDOM_TFLOPS, 4),
                 "kernel": flash_attn_hip.fwd_kernel_name(B, H, D, S, S, dtype), "avg_kernel_ms": round(avg_ms, 4),
@@ -281,8 +287,9 @@ def main():
         rbytes = 2 * 2 * 8 * 2048 * 12 * 64 * 2
         extra["rotary_qkv_inplace_B8_S2048_H12_D64_bf16"] = {
             "ms": round(ms_r, 4), "GBps": round(rbytes / ms_r / 1e6, 1), "frac_hbm": round(rbytes / ms_r / 1e6 / PEAK_HBM_GBS, 4)}
-        # rotary fused into the attention forward (FlashMHA's path: q rotated at the kernel's Q load,
-        # k by a half-size pass) against a separate q+k pass followed by the plain forward. Both legs
+        # rotary attention through FlashMHA's autograd function (FlashAttnRotaryQKVFunc: one q+k rotary
+        # pass + the assembly forward; the HIP forward's Q-load rotation only where no assembly kernel
+        # serves the shape) against a hand-written separate q+k pass followed by the plain forward. Both legs
         # read the same pristine qkv (an in-place pass repeated thousands of times drifts the data,
         # and the softmax's rescale branch makes the kernel time data-dependent): the separate pass
         # writes rotated q, k to a scratch buffer (same bytes as in place).

@@ -137,6 +137,8 @@ NETMP = 16             # rotating exp temporaries
 V_ORT = None           # OR-test accumulator (None: V_TMP[X])
 V_EPT = None           # epilogue temporaries (None: V_TMP[X])
 PRIO4 = False          # 8 waves: s_setprio 1 for waves 4-7 (the SIMD partners dispatched second)
+STAGGER = False        # 8 waves: waves 4-7 run half a tile behind (their barrier mid-tile; ring 6)
+FIRST_MAX_W8 = False   # 8 waves: FIRST_MAX (tile 0's row max sets the starting shift) as in the 4-wave form
 
 
 def rq(base):
@@ -754,7 +756,8 @@ class Gen:
         the shift, S_B(0) is recomputed by tile 0's QK_B with the new seed. Only when tile 0 is
         unmasked for every row (S_MSTART > 0): a masked first tile keeps the initial state (the
         max over keys a row may not see could shift its P out of range)."""
-        out = self.qk('B', 0)
+        # (8 waves: one block per wave, S_A(0) only; its QK(1) runs in phase 0)
+        out = self.qk('B', 0) if NWAVES == 4 else []
         out.append(Inst(f's_cmp_lg_u32 s{S_MSTART}, 0', 'salu', 2, rd=[f's{S_MSTART}']))
         out.append(Inst('s_cselect_b64 s[96:97], -1, 0', 'salu', 2, wr=['s96', 's97']))
         for X in BLOCKS:
@@ -774,6 +777,8 @@ class Gen:
                 out.append(V(f'v_add_f32 v{T + 7}, {ORDET_DELTA[self.dtype]!r}, v{T + 7}', T + 7, [T + 7]))
                 out.append(Inst(f'v_cndmask_b32 v{mc}, v{mc}, v{T + 7}, s[96:97]', 'valu', 4,
                                 rd=[f'v{mc}', f'v{T + 7}', 's96', 's97'], wr=[f'v{mc}']))
+                if MC_BANKS:
+                    out += [V(f'v_mov_b32 v{c}, v{mc}', c, [mc]) for c in range(V_MCB[X], V_MCB[X] + 4)]
         return out
 
     def scale_acc(self, X):
@@ -1588,7 +1593,7 @@ def prologue_sections(g):
     # R 4 / DIST 3 (tile 0 DMAs K4 into slot 0) needs this one, R 6 / DIST 3 with BAR2 does not
     kbar = [raw('s_barrier')] if R - 1 - DIST < (2 if BAR2 else 1) or NWAVES == 8 else []
     p += g.kreads(0) + [raw('s_waitcnt lgkmcnt(0)')] + kbar + g.qk('A', 0)
-    if FIRST_MAX and NWAVES == 4 and ORDET:
+    if FIRST_MAX and ORDET and (NWAVES == 4 or FIRST_MAX_W8):
         p += g.first_max()
     if NWAVES == 8:
         # K1 into the single K buffer behind QK(0) (phase 0 runs QK(1))
@@ -1710,9 +1715,13 @@ PRESCALE_PRODUCT = {'bf16': False, 'f16': False}
 def set_persist(on):
     """Persistent form on/off (D = 64, 4 waves): 8 more kernel-argument bytes (grid size at 168),
     registers up to V_TID."""
-    global PERSIST, KARG_BYTES, NVGPR, V_TID, PERSIST_Q, N_STORES
+    global PERSIST, KARG_BYTES, NVGPR, V_TID, PERSIST_Q, N_STORES, V_MCB
     if on:
-        assert NWAVES == 4 and not MC_BANKS
+        assert NWAVES == 4
+        if MC_BANKS:
+            # the m*c copies move out of the next-Q registers (v168..) to v212.. (PRESCALE's seeds)
+            assert not PRESCALE and D <= 64
+            V_MCB = {'A': 212, 'B': 216}
         # D = 128: Q, row sums and the indicator fill the VGPRs (no room for the next Q): K/V tail
         # only, the workitem id in the last free VGPR
         PERSIST_Q = D <= 64
@@ -2000,28 +2009,50 @@ def tile_phases(g, t, **kw):
     return g.phase1(t, **kw) + g.phase2(t, **kw)
 
 
-def masked_tile(g, t, rescue):
+def stagger_split(lst):
+    """STAGGER (8 waves): a phase's instruction list cut after its first half of MFMAs, and the
+    count of LDS-DMA pieces in the first part (the group-1 barrier's vmcnt)."""
+    mf = [i for i, x in enumerate(lst) if x.kind == 'mfma']
+    cut = mf[len(mf) // 2 - 1] + 1
+    return lst[:cut], lst[cut:], sum(1 for x in lst[:cut] if x.kind == 'dma')
+
+
+def tile_body(g, t, sfx, **kw):
+    """One tile's phases and its barrier. Group 0 (sfx ''): phases, wait, barrier. Group 1 of the
+    STAGGER form (sfx '_g1', waves 4-7): the barrier in the middle of the phase, so these waves run
+    half a tile behind their SIMD partners (MI355X_MICROARCH.md "Two waves per SIMD" item 9). At the
+    group-1 barrier of tile t every DMA piece of tiles < t has landed (vmcnt = the pieces issued
+    before it in this phase), as at the group-0 barrier; the 6-slot ring keeps every slot a DMA
+    rewrites at least two tiles behind the half-tile-late reads (configure_stagger)."""
+    ph = tile_phases(g, t, **kw)
+    if not sfx:
+        return ph + [raw(f's_waitcnt vmcnt({tile_vmcnt()})'), raw('s_barrier')]
+    a, b, n = stagger_split(ph)
+    return a + [raw(f's_waitcnt vmcnt({n})'), raw('s_barrier')] + b
+
+
+def masked_tile(g, t, rescue, sfx=''):
     """Loop position t of the masked loop: tiles from S_MSTART (the causal diagonal band) up to
     the last one, which exits to .Llast{t}."""
-    blk = [label(f'.Lmask{t}'), S(f's_cmp_eq_u32 s{S_J}, s{S_LAST}'), raw(f's_cbranch_scc1 .Llast{t}')]
+    blk = [label(f'.Lmask{sfx}{t}'), S(f's_cmp_eq_u32 s{S_J}, s{S_LAST}'), raw(f's_cbranch_scc1 .Llast{sfx}{t}')]
     blk += nvrel_insts()
-    blk += tile_phases(g, t, masked=True, rescue=rescue)
-    blk += [raw(f's_waitcnt vmcnt({tile_vmcnt()})'), raw('s_barrier'), S(f's_add_u32 s{S_J}, s{S_J}, 1')]
+    blk += tile_body(g, t, sfx, masked=True, rescue=rescue)
+    blk += [S(f's_add_u32 s{S_J}, s{S_J}, 1')]
     if t == U - 1:
-        blk.append(raw('s_branch .Lmask0'))
+        blk.append(raw(f's_branch .Lmask{sfx}0'))
     return blk
 
 
-def last_tile(g, t, rescue, masked=True):
+def last_tile(g, t, rescue, masked=True, sfx=''):
     """Tile t = nt - 1 (position t of the unrolled loop): masked softmax of both blocks, no
     next-tile reads or DMA, then P.V of block B and the two epilogues. LAST_UNMASKED: the masked
     form first tests whether any lane's row sees fewer than all 64 keys of the tile and otherwise
     branches to the unmasked copy (masked=False, .LlastU{t}: key counts that are multiples of 64
     skip 128 compare/select pairs per block)."""
     if not masked:
-        b = [label(f'.LlastU{t}')]
+        b = [label(f'.LlastU{sfx}{t}')]
     else:
-        b = [label(f'.Llast{t}')] + (stamp(STAMP_V + 2) if 'stamps' in PROBE else []) + pstamp(PS_V + 6) + nvrel_insts()
+        b = [label(f'.Llast{sfx}{t}')] + (stamp(STAMP_V + 2) if 'stamps' in PROBE else []) + pstamp(PS_V + 6) + nvrel_insts()
         if LAST_UNMASKED:
             # masked key offsets reach 59 (32 st + 3 + 24): a lane needs the mask iff NVREL < 60
             # (no temporaries: the 8-wave form keeps the previous tile's P in V_TMP)
@@ -2029,10 +2060,10 @@ def last_tile(g, t, rescue, masked=True):
             for i, r in enumerate(nv):
                 b.append(V(f'v_cmp_gt_i32 vcc, 60, v{r}', 'vcc', [r]))
                 last = i == len(nv) - 1
-                b.append(Inst(f's_cbranch_vccz .LlastU{t}' if last else f's_cbranch_vccnz .LlastM{t}', 'br', 4,
+                b.append(Inst(f's_cbranch_vccz .LlastU{sfx}{t}' if last else f's_cbranch_vccnz .LlastM{sfx}{t}', 'br', 4,
                               rd=['vcc']))
             if len(nv) > 1:
-                b.append(label(f'.LlastM{t}'))
+                b.append(label(f'.LlastM{sfx}{t}'))
     b += tile_phases(g, t, masked=masked, last=True, rescue=rescue)
     if NWAVES == 8:
         b += [mark()] + place(g.pv_sum(par(t), t)[0], [])
@@ -2057,6 +2088,10 @@ def build(g):
     if DUMP and DUMP[0] == 'pro':
         pro += dump_block(DUMP[1])
     tiles = []
+    if STAGGER:
+        assert NWAVES == 8 and not PERSIST
+        # waves 4-7 branch to their own copy of the loops (the barrier mid-tile: tile_body)
+        pro += [S(f's_cmp_ge_u32 s{S_WAVE}, 4'), raw('s_cbranch_scc1 .Lloop_g1')]
     for t in range(U):
         blk = []
         if t == 0:
@@ -2066,7 +2101,12 @@ def build(g):
             blk += [S(f's_cmp_eq_u32 s{S_J}, s{S_TAIL}'), raw('s_cbranch_scc1 .Ltail')]
         blk += [S(f's_cmp_ge_u32 s{S_J}, s{S_MSTART}'), raw(f's_cbranch_scc1 .Lmask{t}')]
         if NWAVES == 8:
-            blk += g.phase_w8(t, rescue=rescue)
+            blk += tile_body(g, t, '', rescue=rescue)
+            blk += [S(f's_add_u32 s{S_J}, s{S_J}, 1')]
+            if t == U - 1:
+                blk.append(raw('s_branch .Lloop'))
+            tiles.append(blk)
+            continue
         else:
             blk += g.phase1(t, rescue=rescue)
             if DUMP and DUMP[0] == 'p1' and t == 0:
@@ -2083,8 +2123,20 @@ def build(g):
     masks = [masked_tile(g, t, rescue) for t in range(U)]
     lasts = [last_tile(g, t, rescue) for t in range(U)]
     lastsu = [last_tile(g, t, rescue, masked=False) for t in range(U)] if LAST_UNMASKED else []
+    tiles1, masks1, lasts1, lastsu1 = [], [], [], []
+    if STAGGER:
+        for t in range(U):
+            blk = [raw('.p2align 6'), label('.Lloop_g1')] if t == 0 else []
+            blk += [S(f's_cmp_ge_u32 s{S_J}, s{S_MSTART}'), raw(f's_cbranch_scc1 .Lmask_g1{t}')]
+            blk += tile_body(g, t, '_g1', rescue=rescue) + [S(f's_add_u32 s{S_J}, s{S_J}, 1')]
+            if t == U - 1:
+                blk.append(raw('s_branch .Lloop_g1'))
+            tiles1.append(blk)
+        masks1 = [masked_tile(g, t, rescue, sfx='_g1') for t in range(U)]
+        lasts1 = [last_tile(g, t, rescue, sfx='_g1') for t in range(U)]
+        lastsu1 = [last_tile(g, t, rescue, masked=False, sfx='_g1') for t in range(U)] if LAST_UNMASKED else []
 
-    def last_paths(t):
+    def last_paths(t, lasts=lasts, lastsu=lastsu):
         """The last tile at loop position t: the masked form, and (LAST_UNMASKED) its test then
         the unmasked copy."""
         out = [lambda: refs(lasts[t])]
@@ -2162,10 +2214,22 @@ def build(g):
             for lp in last_paths(t):
                 paths.append(lambda t=t, lp=lp: refs(pro) + seq(tiles[:t]) + [(masks[t], k) for k in range(3)] + lp())
         paths.append(lambda: refs(pro) + refs(empty))
+        if STAGGER:
+            # group 1 (waves 4-7): the same paths through its own loop copies
+            for tl, ms, ls, lu in ((tiles1, masks1, lasts1, lastsu1),):
+                paths.append(lambda: refs(pro) + seq(tl) + seq(tl))
+                for t in range(U):
+                    paths.append(lambda t=t: refs(pro) + seq(tl) + seq(tl[:t]) + seq(ms[t:]) + seq(ms))
+                    for lp in last_paths(t, ls, lu):
+                        paths.append(lambda t=t, lp=lp: refs(pro) + seq(tl) + seq(ms) + seq(ms[:t]) + lp())
+                    paths.append(lambda t=t: refs(pro) + seq(tl[:t]) + seq(ms[t:]) + seq(ms))
+                    for lp in last_paths(t, ls, lu):
+                        paths.append(lambda t=t, lp=lp: refs(pro) + seq(tl[:t]) + [(ms[t], k) for k in range(3)] + lp())
     # rescale blocks entered from their branch: the 40 instructions before it, the block, the rest
     def resc_path(rb):
         ret = rb[-1].txt.split()[-1]
-        for blk in tiles + masks + lasts + lastsu + ([tail] if PERSIST and tail else []):
+        for blk in tiles + masks + lasts + lastsu + tiles1 + masks1 + lasts1 + lastsu1 + \
+                ([tail] if PERSIST and tail else []):
             for i, x in enumerate(blk):
                 if x.kind == 'br' and x.txt.endswith(f'{ret}:'):
                     lo = max(0, i - 40)
@@ -2178,7 +2242,7 @@ def build(g):
         return [pro_a, pb1, qcopy, qload] + pb2 + tiles + masks + lasts + lastsu + [empty, end, done, pb2k] + \
             ([tail] if tail else []) + rescue, n
     n = fix_paths(paths)
-    blocks = [pro] + tiles + masks + lasts + lastsu + [empty, end] + rescue
+    blocks = [pro] + tiles + masks + lasts + lastsu + tiles1 + masks1 + lasts1 + lastsu1 + [empty, end] + rescue
     return blocks, n
 
 
@@ -2255,6 +2319,8 @@ def main():
     ap.add_argument('--hd', type=int, default=64, choices=[32, 64, 96, 128], help='head-dim tile')
     ap.add_argument('--waves', type=int, default=4, choices=[4, 8], help='waves per workgroup (8: D = 64 only)')
     ap.add_argument('--prio4', type=int, default=None, help='8 waves: s_setprio 1 for waves 4-7')
+    ap.add_argument('--stagger', type=int, default=0, help='8 waves: waves 4-7 half a tile behind (ring 6)')
+    ap.add_argument('--fmax8', type=int, default=0, help="8 waves: tile 0's row max sets the starting shift")
     ap.add_argument('--persist', type=int, default=0, help='persistent workgroups: next-block K/V tail (and next-Q prefetch at D = 64), 4 waves')
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats', action='store_true')
@@ -2312,9 +2378,10 @@ def main():
     global ORDET, EXP_LAG, CVT_LAG, MC_BANKS, NVGPR
     if args.ordet is not None:
         ORDET = bool(args.ordet)
-    if args.lag:
+    # (--lag and --mcbanks tune the 4-wave softmax stream; the 8-wave form keeps its own settings)
+    if args.lag and NWAVES == 4:
         EXP_LAG, CVT_LAG = (int(x) for x in args.lag.split(','))
-    if args.mcbanks is not None:
+    if args.mcbanks is not None and NWAVES == 4 and V_MCB is not None:
         MC_BANKS = bool(args.mcbanks)
     global KFIRST, KFIRST_LO, LGKM_XPHASE, PRESCALE, PHASE_TAIL
     if args.ptail is not None:
@@ -2339,9 +2406,15 @@ def main():
         KFIRST, KFIRST_LO = args.kfirst > 0, max(0, args.kfirst)
     if args.xphase is not None:
         LGKM_XPHASE = bool(args.xphase)
-    global PRIO4
+    global PRIO4, STAGGER
     if args.prio4 is not None:
         PRIO4 = bool(args.prio4)
+    if args.stagger and NWAVES == 8:     # (ignored by the 4-wave forms: variant-library builds)
+        STAGGER = True
+    global FIRST_MAX_W8
+    if args.fmax8 and NWAVES == 8:
+        FIRST_MAX_W8 = True
+        set_geometry(6, 3)
     set_persist(bool(args.persist))
     set_prescale(prescale)
     if MC_BANKS:
