@@ -139,6 +139,7 @@ V_EPT = None           # epilogue temporaries (None: V_TMP[X])
 PRIO4 = False          # 8 waves: s_setprio 1 for waves 4-7 (the SIMD partners dispatched second)
 STAGGER = False        # 8 waves: waves 4-7 run half a tile behind (their barrier mid-tile; ring 6)
 FIRST_MAX_W8 = False   # 8 waves: FIRST_MAX (tile 0's row max sets the starting shift) as in the 4-wave form
+STAGGER_FRAC = 0.5     # STAGGER: the group-1 barrier after this fraction of a phase's MFMAs
 
 
 def rq(base):
@@ -1766,7 +1767,7 @@ def prologue_persist(g):
         # the prefetched Q is scaled on its way into the AGPRs (no AGPR pass at .Lqdone), after this
         # block's first DMAs are issued: its ~800 cycles run under their latency (QCOPY_LATE)
         qc = q_prescale(g, src=[(V_QN + 16 * xi + r, A_Q[X] + r) for xi, X in enumerate(BLOCKS)
-                                for r in range(16)]) + pstamp(PS_V + 4, 'pstB')
+                                for r in range(16)])
         if QCOPY_LATE:
             qcopy, qcopy_late = [raw('s_branch .Lqdone')], qc
         else:
@@ -1817,7 +1818,12 @@ def prologue_persist(g):
         qs = [S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqfirst')]
         qcb = qcopy_late + [raw('s_branch .Lqsdone')]
         qfb = [label('.Lqfirst')] + sc['qscale']
-    pb2 = [label('.Lqdone'), S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + sc['dma'] + qs + pf + \
+    # 'pstB' probe: the loop-start stamp at .Lqdone, which the first block (after its Q loads) and every
+    # later block (after the next-Q copy) pass. (Round 4 stamped inside the later blocks' copy only, so
+    # the first block of every workgroup never wrote it: the negative round-0 prologues of
+    # profiles/r04_pstamps/pstamps_r04f/h.)
+    pb2 = [label('.Lqdone')] + pstamp(PS_V + 4, 'pstB') + [S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + \
+        sc['dma'] + qs + pf + \
         sc['zero'] + start_with_wait(start_pieces() + nq)
     if qcb is not None:
         # pb2 as [head up to the branch, the copy, the first-block scale, the rest from .Lqsdone]
@@ -2013,7 +2019,8 @@ def stagger_split(lst):
     """STAGGER (8 waves): a phase's instruction list cut after its first half of MFMAs, and the
     count of LDS-DMA pieces in the first part (the group-1 barrier's vmcnt)."""
     mf = [i for i, x in enumerate(lst) if x.kind == 'mfma']
-    cut = mf[len(mf) // 2 - 1] + 1
+    k = max(1, min(len(mf) - 1, round(len(mf) * STAGGER_FRAC)))
+    cut = mf[k - 1] + 1
     return lst[:cut], lst[cut:], sum(1 for x in lst[:cut] if x.kind == 'dma')
 
 
@@ -2321,6 +2328,8 @@ def main():
     ap.add_argument('--prio4', type=int, default=None, help='8 waves: s_setprio 1 for waves 4-7')
     ap.add_argument('--stagger', type=int, default=0, help='8 waves: waves 4-7 half a tile behind (ring 6)')
     ap.add_argument('--fmax8', type=int, default=0, help="8 waves: tile 0's row max sets the starting shift")
+    ap.add_argument('--sfrac', type=float, default=None, help='STAGGER: group-1 barrier after this fraction of the MFMAs')
+    ap.add_argument('--lag8', default=None, help='8 waves: EXP_LAG,CVT_LAG')
     ap.add_argument('--persist', type=int, default=0, help='persistent workgroups: next-block K/V tail (and next-Q prefetch at D = 64), 4 waves')
     ap.add_argument('--out', required=True)
     ap.add_argument('--stats', action='store_true')
@@ -2411,9 +2420,13 @@ def main():
         PRIO4 = bool(args.prio4)
     if args.stagger and NWAVES == 8:     # (ignored by the 4-wave forms: variant-library builds)
         STAGGER = True
-    global FIRST_MAX_W8
+    global FIRST_MAX_W8, STAGGER_FRAC
     if args.fmax8 and NWAVES == 8:
         FIRST_MAX_W8 = True
+    if args.sfrac is not None:
+        STAGGER_FRAC = args.sfrac
+    if args.lag8 and NWAVES == 8:
+        EXP_LAG, CVT_LAG = (int(x) for x in args.lag8.split(','))
         set_geometry(6, 3)
     set_persist(bool(args.persist))
     set_prescale(prescale)

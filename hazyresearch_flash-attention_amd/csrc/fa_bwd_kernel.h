@@ -35,6 +35,12 @@ namespace fa {
 #ifndef FA_BWD_KV_LDS
 #define FA_BWD_KV_LDS 1         // 1 (D <= 64, causal): K/V B operands re-read from LDS every query tile
 #endif
+#ifndef FA_BWD_RC_ALL
+#define FA_BWD_RC_ALL 0         // 1: every lane of the staging half stages the row constants (no lane branch)
+#endif
+#ifndef FA_BWD_LANE_BASES
+#define FA_BWD_LANE_BASES 1     // 1: LDS reads from loop-invariant lane bases + immediates
+#endif
 
 // Waves per workgroup (32 keys each). dQ atomic bytes scale with 1/NW, so both use 8 at D <= 64
 // (causal: 4-wave blocks balanced the triangle better but were slower once K/V moved to LDS).
@@ -243,6 +249,28 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     const int pp = lane & 3;
     const int g4 = lane >> 4;          // 16-lane group index 0..3 (16x16x32 operands)
 
+    // Loop-invariant LDS lane bases. The D <= 64 swizzles depend on row bits 1..3 (Swz::x, ds_off)
+    // only, so a row offset of 16 or 32 is a plain byte offset that folds into the instruction's
+    // immediate; written this way the compiler keeps a handful of base registers instead of one
+    // computed address per read (which it rematerialized inside the loop under register pressure).
+    static_assert(D <= 64, "row offsets of 16 / 32 are additive for the D <= 64 swizzles");
+    // (D = 32 keeps the per-read expressions: its translation unit's iterative-ILP scheduler
+    // crashes hipcc 7.2 on the lane-base form)
+    constexpr bool LB = FA_BWD_LANE_BASES && D == 64;
+    // (the dropout kernels, at the 256-register limit with the Philox state, recompute the row-read
+    // addresses instead of holding four more registers)
+    int qd_base[D / 16];                                   // Q / dO / K / V row reads, k-step ks
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) qd_base[ks] = S::off(l32, 2 * ks + hi);
+    auto qd_off = [&](int ks) __attribute__((always_inline)) -> int {
+        return (DROPOUT || !LB) ? S::off(l32, 2 * ks + hi) : qd_base[ks];
+    };
+    int tr_base[2][D / 32];                                // dO^T / Q^T reads: [row +8][d-block]
+#pragma unroll
+    for (int h8 = 0; h8 < 2; ++h8)
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) tr_base[h8][dt] = S::off8(4 * hi + qq + 8 * h8, 32 * dt + 16 * grp + 4 * pp);
+
     const int q_begin = CAUSAL ? k0 : 0;   // rows q < k0 see no key of this block
     const int nqt = seqlen_q > q_begin ? (seqlen_q - q_begin + C::BQ - 1) / C::BQ : 0;
 
@@ -260,6 +288,10 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     const int sl = tid - HALF * stg_half;
     const int crow_ = sl / C::NC, ccol = sl % C::NC;
     const bool chunk_ok = sl < CH && ccol * 8 < head_dim;
+    // every lane of a half takes part in the row-constant staging (row sl % BQ: the 8 lanes of a row
+    // load and store the same values), so no lane-divergent branch wraps it
+    const int crow_c = FA_BWD_RC_ALL ? sl % C::BQ : sl;
+    const bool rc_lane = FA_BWD_RC_ALL || sl < C::BQ;   // lanes that stage the row constants
     u32x4 qst = {0u, 0u, 0u, 0u}, dst = {0u, 0u, 0u, 0u};
     float lse_st = 0.f, del_st = 0.f;
     const auto q_rs = make_rsrc_n(qp, seqlen_q * (int)a.q_row_stride * 2);
@@ -267,39 +299,42 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     const int qld_off = chunk_ok ? (crow_ * (int)a.q_row_stride + ccol * 8) * 2 : OOB;
     const int dold_off = chunk_ok ? (crow_ * (int)a.do_row_stride + ccol * 8) * 2 : OOB;
     const int st_off = S::off(crow_, ccol);
+    const int cb = k0 >> 8;
+    auto row_live = [&](int r) __attribute__((always_inline)) -> bool {
+        return r < bm.rows && bm.mask[(int64_t)r * bm.row_stride + cb] != 0;
+    };
     auto gload_qtile = [&](int q0n) __attribute__((always_inline)) {
-        if (sl < CH) {
+        if (CH == HALF || sl < CH) {
             qst = bload128s(q_rs, qld_off, q0n * (int)a.q_row_stride * 2);
             dst = bload128s(do_rs, dold_off, q0n * (int)a.do_row_stride * 2);
         }
-        // unconditional loads of a clamped row, used only at the LDS write (rows past seqlen_q
-        // are masked to P = 0 whatever their constants)
-        if (sl < C::BQ) {
-            const int qc = min(q0n + sl, seqlen_q - 1);
+        // row constants of a clamped row (rows past seqlen_q get lse = +inf at the LDS write, so
+        // their P = exp2(s c - inf) = 0 with no per-element mask)
+        if (rc_lane) {
+            const int qc = min(q0n + crow_c, seqlen_q - 1);
             lse_st = lse_g[qc];
             del_st = del_g[qc];
         }
     };
-    auto lds_store_qtile = [&](int buf) __attribute__((always_inline)) {
-        if (sl < CH) {
+    auto lds_store_qtile = [&](int buf, int q0n) __attribute__((always_inline)) {
+        if (CH == HALF || sl < CH) {
             lds_write128(smem + C::OFF_Q + buf * C::Q_IMG, st_off, qst);
             lds_write128(smem + C::OFF_DO + buf * C::Q_IMG, st_off, dst);
         }
-        if (sl < C::BQ) {
-            // one lane offset for both rows' constants (the image offsets fold into the
-            // instruction), so no per-buffer address stays live across the loop
-            lds_write32(smem + C::OFF_LSE + buf * C::BQ * 4, 4 * sl, lse_st * LOG2E);
-            lds_write32(smem + C::OFF_DELTA + buf * C::BQ * 4, 4 * sl, -del_st);   // -delta
+        // one lane offset for both rows' constants (the image offsets fold into the instruction).
+        // Rows past seqlen_q and (block-sparse) dead 16-row halves get lse = +inf: P = 0 there.
+        if (rc_lane) {
+            const int qr = q0n + crow_c;
+            bool dead = qr >= seqlen_q;
+            if constexpr (SPARSE) dead = dead || !row_live(qr >> 4);
+            lds_write32(smem + C::OFF_LSE + buf * C::BQ * 4, 4 * crow_c, dead ? INFINITY : lse_st * LOG2E);
+            lds_write32(smem + C::OFF_DELTA + buf * C::BQ * 4, 4 * crow_c, -del_st);   // -delta
         }
     };
     // ---- block sparsity (fa_bwd_block): this workgroup's keys lie in one 256-key column block
     // cb; a 32-row query tile is live when either of its 16-row blocks is 1 in column cb. The
     // live tiles are kept as a bit set in LDS and walked in order; dead tiles are never loaded.
     uint64_t *qlive = (uint64_t *)(smem + C::OFF_QLIVE);
-    const int cb = k0 >> 8;
-    auto row_live = [&](int r) __attribute__((always_inline)) -> bool {
-        return r < bm.rows && bm.mask[(int64_t)r * bm.row_stride + cb] != 0;
-    };
     if constexpr (SPARSE) {
         for (int chunk = wave; chunk < C::QLIVE_WORDS; chunk += C::NW) {
             const int t = 64 * chunk + lane;
@@ -333,7 +368,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     if (t_first < nqt) {
         if (stg_half == 0) {
             gload_qtile(q_begin + t_first * C::BQ);
-            lds_store_qtile(0);
+            lds_store_qtile(0, q_begin + t_first * C::BQ);
         } else if (t_second < nqt) {
             gload_qtile(q_begin + t_second * C::BQ);
         }
@@ -345,7 +380,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     // are dealt round-robin to the waves, each summing over every key of the block, so one fp32
     // atomic per element per block. store_buf >= 0: the waves holding a dQ tile write the staged
     // query tile into LDS buffer store_buf before their atomics.
-    auto dq_phase = [&](const char *dsr, int qd, int store_buf) __attribute__((always_inline)) {
+    auto dq_phase = [&](const char *dsr, int qd, int store_buf, int store_q0) __attribute__((always_inline)) {
 #pragma unroll
         for (int t0 = 0; t0 < 2 * (D / 16); t0 += C::NW) {
             const int t = t0 + wave;
@@ -353,13 +388,16 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                 const int qh = t & 1;
                 const int dbase = 16 * (t >> 1);
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                // rows r0 = 32 ks + 8 g4 + qq (+4): key step ks is an immediate offset (32 rows)
+                const int ds0 = ds_off(8 * g4 + qq, 16 * qh + 4 * pp), ds1 = ds_off(8 * g4 + qq + 4, 16 * qh + 4 * pp);
+                const int kb0 = S::off8(8 * g4 + qq, dbase + 4 * pp), kb1 = S::off8(8 * g4 + qq + 4, dbase + 4 * pp);
                 auto dq_operands = [&](int ks, u32x4 &av, u32x4 &bv) __attribute__((always_inline)) {
                     const int r0 = 32 * ks + 8 * g4 + qq;
-                    u32x2 a0 = lds_read_tr(dsr, ds_off(r0, 16 * qh + 4 * pp));
-                    u32x2 a1 = lds_read_tr(dsr, ds_off(r0 + 4, 16 * qh + 4 * pp));
+                    u32x2 a0 = lds_read_tr(dsr, LB ? ds0 + 32 * ks * 64 : ds_off(r0, 16 * qh + 4 * pp));
+                    u32x2 a1 = lds_read_tr(dsr, LB ? ds1 + 32 * ks * 64 : ds_off(r0 + 4, 16 * qh + 4 * pp));
                     av = u32x4{a0[0], a0[1], a1[0], a1[1]};
-                    u32x2 b0 = lds_read_tr(kimg, S::off8(r0, dbase + 4 * pp));
-                    u32x2 b1 = lds_read_tr(kimg, S::off8(r0 + 4, dbase + 4 * pp));
+                    u32x2 b0 = lds_read_tr(kimg, LB ? kb0 + 32 * ks * S::ROW_BYTES : S::off8(r0, dbase + 4 * pp));
+                    u32x2 b1 = lds_read_tr(kimg, LB ? kb1 + 32 * ks * S::ROW_BYTES : S::off8(r0 + 4, dbase + 4 * pp));
                     bv = u32x4{b0[0], b0[1], b1[0], b1[1]};
                 };
                 // operands of key step ks+1 are read before the MFMA of step ks
@@ -376,7 +414,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                 // the staged query tile goes to LDS first: its vmcnt wait then covers only loads
                 // (vmcnt retires in issue order), and these atomics have a whole tile of compute
                 // before the next wait
-                if (t0 == 0 && store_buf >= 0) lds_store_qtile(store_buf);
+                if (t0 == 0 && store_buf >= 0) lds_store_qtile(store_buf, store_q0);
                 if (qd + C::BQ <= seqlen_q && head_dim == D) {
                     // full tile (wave-uniform test): the four atomics without per-lane guards
                     float *base = dqa + (int64_t)(qd + 16 * qh + 4 * g4) * dqa_row + d;
@@ -412,9 +450,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         const int q0 = q_begin + it * C::BQ;
         char *dsw = dsimg + BUF * C::DS_IMG;
         if (my_load && itnn < nqt) gload_qtile(q_begin + itnn * C::BQ);
-        // block sparsity: a dead 16-row half of a live tile is masked (P = 0 there)
-        const bool dead0 = SPARSE && !row_live(q0 >> 4);
-        const bool dead1 = SPARSE && !row_live((q0 >> 4) + 1);
+        // (block sparsity: a dead 16-row half of a live tile has lse = +inf in its row constants)
         const bool active = !CAUSAL || (q0 + C::BQ - 1 >= kw);
         u32x4 pk[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}}, sk[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
         // ---- dV^T += dO^T Pd ; dK^T += Q^T dS  (A operands by transposed reads). Causal kernels
@@ -426,16 +462,18 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         auto dvdk = [&]() __attribute__((always_inline)) {
 #pragma unroll
             for (int sg = 0; sg < 2; ++sg) {
-                const int rb = 16 * sg + 4 * hi + qq;
+                const int ro = 16 * sg * S::ROW_BYTES;    // rows 16 sg + 4 hi + qq (+8)
 #pragma unroll
                 for (int dt = 0; dt < D / 32; ++dt) {
-                    const int col = 32 * dt + 16 * grp + 4 * pp;
-                    u32x2 a0 = lds_read_tr(doimg, S::off8(rb, col));
-                    u32x2 a1 = lds_read_tr(doimg, S::off8(rb + 8, col));
+                    const int rb = 16 * sg + 4 * hi + qq, col = 32 * dt + 16 * grp + 4 * pp;
+                    const int o0 = LB ? tr_base[0][dt] + ro : S::off8(rb, col);
+                    const int o1 = LB ? tr_base[1][dt] + ro : S::off8(rb + 8, col);
+                    u32x2 a0 = lds_read_tr(doimg, o0);
+                    u32x2 a1 = lds_read_tr(doimg, o1);
                     u32x4 av = {a0[0], a0[1], a1[0], a1[1]};
                     dv[dt] = T::mfma32(as_frag<T>(av), as_frag<T>(pk[sg]), dv[dt]);
-                    u32x2 b0 = lds_read_tr(qimg, S::off8(rb, col));
-                    u32x2 b1 = lds_read_tr(qimg, S::off8(rb + 8, col));
+                    u32x2 b0 = lds_read_tr(qimg, o0);
+                    u32x2 b1 = lds_read_tr(qimg, o1);
                     u32x4 bv = {b0[0], b0[1], b1[0], b1[1]};
                     dk[dt] = T::mfma32(as_frag<T>(bv), as_frag<T>(sk[sg]), dk[dt]);
                 }
@@ -462,10 +500,10 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             }
 #pragma unroll
             for (int ks = 0; ks < D / 16; ++ks) {
-                u32x4 qa = lds_read128(qimg, S::off(l32, 2 * ks + hi));
-                u32x4 da = lds_read128(doimg, S::off(l32, 2 * ks + hi));
+                u32x4 qa = lds_read128(qimg, qd_off(ks));
+                u32x4 da = lds_read128(doimg, qd_off(ks));
                 if constexpr (C::KV_LDS) {
-                    const int ko = S::off(32 * wave + l32, 2 * ks + hi);
+                    const int ko = qd_off(ks) + 32 * wave * S::ROW_BYTES;   // row 32 wave + l32
                     sacc = T::mfma32(as_frag<T>(qa), as_frag<T>(lds_read128(kimg, ko)), sacc);
                     zacc = T::mfma32(as_frag<T>(da), as_frag<T>(lds_read128(smem + C::OFF_V, ko)), zacc);
                 } else {
@@ -473,9 +511,11 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                     zacc = T::mfma32(as_frag<T>(da), vf[ks], zacc);
                 }
             }
-            // row constants for rows crow(4g+e, hi) = 8g + 4hi + e (16-B aligned groups of 4)
-            const bool need_mask = (q0 + C::BQ > seqlen_q) || (k0 + C::BKV > seqlen_k) ||
-                                   (CAUSAL && q0 < kw + 31) || dead0 || dead1;
+            // Rows past seqlen_q and dead (block-sparse) rows carry lse = +inf in the staged row
+            // constants, so their P is 0 with no test here; only the last key block (keys past
+            // seqlen_k) and the causal diagonal tiles take the per-element mask, as a separate copy
+            // of the loop behind one wave-uniform branch (no select on every tile).
+            const bool need_mask = (k0 + C::BKV > seqlen_k) || (CAUSAL && q0 < kw + 31);
             u32x4 rw[2];
             if (DROPOUT) {
 #pragma unroll
@@ -486,34 +526,39 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             }
             // P and dS in place: sacc -> Pd (dropped, scaled P), zacc -> dS. Row constants for
             // rows crow(4g+e, hi) = 8g + 4hi + e are one 16-B LDS read per group of 4 registers.
+            auto pds = [&](auto masked_tag) __attribute__((always_inline)) {
+                constexpr bool MASKED = decltype(masked_tag)::value;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 lse4 = *reinterpret_cast<const f32x4 *>(lse_b + 8 * g + 4 * hi);
-                const f32x4 del4 = *reinterpret_cast<const f32x4 *>(del_b + 8 * g + 4 * hi);
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 lse4 = *reinterpret_cast<const f32x4 *>(lse_b + 8 * g + 4 * hi);
+                    const f32x4 del4 = *reinterpret_cast<const f32x4 *>(del_b + 8 * g + 4 * hi);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int r = 4 * g + e;
-                    float p = fast_exp2(fmaf(sacc[r], c_log2, -lse4[e]));
-                    if (need_mask) {
-                        const int q = q0 + crow(r, hi);
-                        if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q) || (r < 8 ? dead0 : dead1))
-                            p = 0.f;
+                    for (int e = 0; e < 4; ++e) {
+                        const int r = 4 * g + e;
+                        float p = fast_exp2(fmaf(sacc[r], c_log2, -lse4[e]));
+                        if constexpr (MASKED) {
+                            if (kvrow >= seqlen_k || (CAUSAL && kvrow > q0 + crow(r, hi))) p = 0.f;
+                        }
+                        float dpv = zacc[r];
+                        float pdv = p;
+                        if (DROPOUT) {
+                            const int slot = (r & 3) | (((r >> 2) & 1) << 2);
+                            const uint32_t word = rw[r >> 3][slot >> 1];
+                            const uint32_t rnd = (slot & 1) ? (word >> 16) : (word & 0xFFFFu);
+                            // one select: the kept scale 1/(1-p) or 0, then two multiplies
+                            const float rpk = rnd <= keep_thr ? rp : 0.f;
+                            dpv = dpv * rpk;
+                            pdv = p * rpk;
+                        }
+                        sacc[r] = pdv;
+                        zacc[r] = SEED_DZ ? p * dpv : p * (dpv + del4[e]);
                     }
-                    float dpv = zacc[r];
-                    float pdv = p;
-                    if (DROPOUT) {
-                        const int slot = (r & 3) | (((r >> 2) & 1) << 2);
-                        const uint32_t word = rw[r >> 3][slot >> 1];
-                        const uint32_t rnd = (slot & 1) ? (word >> 16) : (word & 0xFFFFu);
-                        // one select: the kept scale 1/(1-p) or 0, then two multiplies
-                        const float rpk = rnd <= keep_thr ? rp : 0.f;
-                        dpv = dpv * rpk;
-                        pdv = p * rpk;
-                    }
-                    sacc[r] = pdv;
-                    zacc[r] = SEED_DZ ? p * dpv : p * (dpv + del4[e]);
                 }
-            }
+            };
+            if (__builtin_amdgcn_readfirstlane((int)need_mask))
+                pds(std::true_type{});
+            else
+                pds(std::false_type{});
             // packed 16-bit Pd and dS: the B operands of dV^T / dK^T and the dS image words
 #pragma unroll
             for (int sg = 0; sg < 2; ++sg)
@@ -540,12 +585,12 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             // that closed the previous step, so each step needs a single barrier (the dS image of
             // this tile is read in the next step, the other buffer)
             if (itp >= 0) {
-                dq_phase(dsimg + (1 - BUF) * C::DS_IMG, q_begin + itp * C::BQ, store_buf);
+                dq_phase(dsimg + (1 - BUF) * C::DS_IMG, q_begin + itp * C::BQ, store_buf, q_begin + itn * C::BQ);
                 stored = true;
             }
         }
         // waves without a dQ tile (or steps without a dQ phase) store the staged tile here
-        if (store_buf >= 0 && !(stored && wave < 2 * (D / 16))) lds_store_qtile(store_buf);
+        if (store_buf >= 0 && !(stored && wave < 2 * (D / 16))) lds_store_qtile(store_buf, q_begin + itn * C::BQ);
         __syncthreads();
     };
     int ilast = -1, blast = 0;   // last tile and its buffer (its dQ runs after the walk)
@@ -578,9 +623,9 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         // dQ of the last tile (its dS image is complete since the last step's closing barrier)
         if (ilast >= 0) {
             if (blast)
-                dq_phase(dsimg + C::DS_IMG, q_begin + ilast * C::BQ, -1);
+                dq_phase(dsimg + C::DS_IMG, q_begin + ilast * C::BQ, -1, 0);
             else
-                dq_phase(dsimg, q_begin + ilast * C::BQ, -1);
+                dq_phase(dsimg, q_begin + ilast * C::BQ, -1, 0);
         }
     }
 

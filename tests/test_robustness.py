@@ -189,15 +189,23 @@ ref, _ = attention_ref(qb, kb, vb)
 pt, _ = attention_ref(qb, kb, vb, upcast=False, reorder_ops=True)
 err = (out.view(B, S, H, d).float() - ref.float()).abs().max().item()
 assert err <= max_err_bound(pt, ref), err
-eager = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
+eager = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)     # AUTO: the assembly kernel
+from flash_attn import flash_attn_hip as hip
+with hip.force_impl(hip.FA_IMPL_HIP):
+    hip_out = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
 torch.cuda.synchronize()
-print("ok", err, bool(torch.equal(eager, out)))
+assert hip.fwd_kernel_name(B, H, d, S, S, torch.bfloat16).endswith("_asm")
+assert not torch.equal(eager, hip_out)      # the two families differ in the last bits here
+path = "asm" if torch.equal(eager, out) else "hip" if torch.equal(hip_out, out) else "neither"
+print("ok", err, path)
 """
 
 
 def test_first_forward_of_a_process_inside_graph_capture():
-    """a fresh process whose first forward is captured (the asm code objects are
-    loaded inside the capture, or the call falls back to the HIP kernels) replays correctly."""
+    """a fresh process whose first forward is captured replays correctly, and
+    the captured launch is the assembly kernel (its code objects load inside the capture, in relaxed
+    capture mode: fa_asm.cpp load_all), bitwise equal to an eager AUTO call and not to the HIP
+    fallback's output."""
     import os
     import subprocess
     import sys
@@ -206,4 +214,5 @@ def test_first_forward_of_a_process_inside_graph_capture():
     r = subprocess.run([sys.executable, "-c", _FRESH_CAPTURE, pkg, root], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert r.stdout.strip().splitlines()[-1].startswith("ok")
+    last = r.stdout.strip().splitlines()[-1].split()
+    assert last[0] == "ok" and last[-1] == "asm", last
