@@ -38,6 +38,11 @@ namespace fa {
 #ifndef FA_BWD_RC_ALL
 #define FA_BWD_RC_ALL 0         // 1: every lane of the staging half stages the row constants (no lane branch)
 #endif
+#ifndef FA_BWD_HOIST
+#define FA_BWD_HOIST 1   // 1: S / dZ operands read ahead of their MFMA chains (D = 64, dense)
+#endif
+// per instantiation: C3 (causal, dropout) -2 %, the other D = 64 shapes even, D = 32 even to +2 %
+constexpr bool bwd_hoist(int D, bool sparse) { return FA_BWD_HOIST && !sparse && D == 64; }
 #ifndef FA_BWD_LANE_BASES
 #define FA_BWD_LANE_BASES 1     // 1: LDS reads from loop-invariant lane bases + immediates
 #endif
@@ -498,17 +503,44 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                     for (int e = 0; e < 4; ++e) zacc[4 * g + e] = del4[e];
                 }
             }
+            if constexpr (bwd_hoist(D, SPARSE)) {
+                // every k-step's operands read before the chains, in k-step order (the compiler
+                // otherwise kept one read in flight per MFMA: one exposed LDS latency each)
+                u32x4 qa[D / 16], da[D / 16], ka[D / 16], va[D / 16];
 #pragma unroll
-            for (int ks = 0; ks < D / 16; ++ks) {
-                u32x4 qa = lds_read128(qimg, qd_off(ks));
-                u32x4 da = lds_read128(doimg, qd_off(ks));
-                if constexpr (C::KV_LDS) {
-                    const int ko = qd_off(ks) + 32 * wave * S::ROW_BYTES;   // row 32 wave + l32
-                    sacc = T::mfma32(as_frag<T>(qa), as_frag<T>(lds_read128(kimg, ko)), sacc);
-                    zacc = T::mfma32(as_frag<T>(da), as_frag<T>(lds_read128(smem + C::OFF_V, ko)), zacc);
-                } else {
-                    sacc = T::mfma32(as_frag<T>(qa), kf[ks], sacc);
-                    zacc = T::mfma32(as_frag<T>(da), vf[ks], zacc);
+                for (int ks = 0; ks < D / 16; ++ks) {
+                    qa[ks] = lds_read128(qimg, qd_off(ks));
+                    da[ks] = lds_read128(doimg, qd_off(ks));
+                    if constexpr (C::KV_LDS) {
+                        const int ko = qd_off(ks) + 32 * wave * S::ROW_BYTES;
+                        ka[ks] = lds_read128(kimg, ko);
+                        va[ks] = lds_read128(smem + C::OFF_V, ko);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int ks = 0; ks < D / 16; ++ks) {
+                    if constexpr (C::KV_LDS) {
+                        sacc = T::mfma32(as_frag<T>(qa[ks]), as_frag<T>(ka[ks]), sacc);
+                        zacc = T::mfma32(as_frag<T>(da[ks]), as_frag<T>(va[ks]), zacc);
+                    } else {
+                        sacc = T::mfma32(as_frag<T>(qa[ks]), kf[ks], sacc);
+                        zacc = T::mfma32(as_frag<T>(da[ks]), vf[ks], zacc);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < D / 16; ++ks) {
+                    u32x4 qa = lds_read128(qimg, qd_off(ks));
+                    u32x4 da = lds_read128(doimg, qd_off(ks));
+                    if constexpr (C::KV_LDS) {
+                        const int ko = qd_off(ks) + 32 * wave * S::ROW_BYTES;   // row 32 wave + l32
+                        sacc = T::mfma32(as_frag<T>(qa), as_frag<T>(lds_read128(kimg, ko)), sacc);
+                        zacc = T::mfma32(as_frag<T>(da), as_frag<T>(lds_read128(smem + C::OFF_V, ko)), zacc);
+                    } else {
+                        sacc = T::mfma32(as_frag<T>(qa), kf[ks], sacc);
+                        zacc = T::mfma32(as_frag<T>(da), vf[ks], zacc);
+                    }
                 }
             }
             // Rows past seqlen_q and dead (block-sparse) rows carry lse = +inf in the staged row

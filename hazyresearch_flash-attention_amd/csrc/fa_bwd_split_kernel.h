@@ -59,6 +59,15 @@ struct BwdSplitCfg {
     static constexpr int QCH = (BQ * NC + NT - 1) / NT;
 };
 
+#ifndef FA_BWD_SPLIT_KVL_SKEW
+#define FA_BWD_SPLIT_KVL_SKEW 0   // 0: the skewed kernels keep K / V rows in registers (C4 bwd -3 %, D=128 -4 %)
+#endif
+#ifndef FA_BWD_SPLIT_PROBE
+#define FA_BWD_SPLIT_PROBE 0
+#endif
+#ifndef FA_BWD_SPLIT_HOIST
+#define FA_BWD_SPLIT_HOIST 1  // 1: skewed steps read their row constants and operands ahead, mask unswitched
+#endif
 #ifndef FA_BWD_SPLIT_SKEW
 #define FA_BWD_SPLIT_SKEW 1   // 1: P waves one query tile ahead of dS waves (dense, no dropout, no dQ)
 #endif
@@ -66,10 +75,18 @@ constexpr bool bwd_split_skew(bool dq, bool dropout, bool sparse) {
     return FA_BWD_SPLIT_SKEW && !dq && !dropout && !sparse;
 }
 
+// the configuration of one instantiation (kernel and launcher)
+template <int D, bool CAUSAL, bool DROPOUT, bool SPARSE, bool DQ>
+using BwdSplitCfgOf = BwdSplitCfg<D,
+                                  bwd_split_skew(DQ, DROPOUT, SPARSE)
+                                      ? (bool)FA_BWD_SPLIT_KVL_SKEW
+                                      : (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL,
+                                  bwd_split_skew(DQ, DROPOUT, SPARSE)>;
+
 // DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
 __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a, const FaBlockMask bm, const int slots) {
-    using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL, bwd_split_skew(DQ, DROPOUT, SPARSE)>;
+    using C = BwdSplitCfgOf<D, CAUSAL, DROPOUT, SPARSE, DQ>;
     using S = Swz<D>;
     constexpr float LOG2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -432,7 +449,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
     auto sstep = [&](auto qb_tag, int u) __attribute__((always_inline)) {
         constexpr int QB = decltype(qb_tag)::value;           // buffer of tile u
         constexpr int QBD = (QB + 2) % 3;                      // buffer of tile u-1 (dS waves)
-        if (u + 1 < nqt) gload_qtile(q_begin + (u + 1) * C::BQ);
+        if (u + 1 < nqt && FA_BWD_SPLIT_PROBE != 4) gload_qtile(q_begin + (u + 1) * C::BQ);
         const int tile = role_p ? u : u - 1;
         const int q0 = q_begin + tile * C::BQ;
         const bool has = role_p ? u < nqt : u >= 1;
@@ -443,49 +460,94 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
             const char *doimg = smem + C::OFF_DO + (role_p ? QB : QBD) * C::Q_IMG;
             f32x16 x;
             const char *aimg = role_p ? qimg : doimg;
+            // row constants (lse, or delta and the P image of the tile) issued ahead of the product:
+            // none of them depends on it, and read behind it they exposed one LDS latency per group
+            f32x4 rc4[4];
+            u32x4 pw[4];
+            if (FA_BWD_SPLIT_HOIST) {
+                const float *rcb = role_p ? lse_s + QB * C::BQ : del_s + QBD * C::BQ;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) rc4[g] = *reinterpret_cast<const f32x4 *>(rcb + 8 * g + 4 * hi);
+                if (!role_p) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) pw[j] = lds_read128(pxb, j * 1024 + lane * 16);
+                }
+            }
             // (dZ's accumulator seeded with -delta, as fa_bwd_kernel does without dropout, measured
             // 3-6 % slower in this kernel: C4 backward 4.01 vs 3.77 ms)
 #pragma unroll
             for (int r = 0; r < 16; ++r) x[r] = 0.f;
+            if (FA_BWD_SPLIT_HOIST) {
+                // operands of all D/16 k-steps read before the chain (the compiler otherwise kept one
+                // read in flight per MFMA)
+                typename T::frag qa[D / 16], kv[D / 16];
 #pragma unroll
-            for (int ks = 0; ks < D / 16; ++ks) {
-                const auto qa = as_frag<T>(lds_read128(aimg, S::off(l32, 2 * ks + hi)));
-                if constexpr (C::KVL)
-                    x = T::mfma32(qa, as_frag<T>(lds_read128(role_p ? kimg : smem + C::OFF_V,
-                                                             S::off(32 * kwave + l32, 2 * ks + hi))), x);
-                else
-                    x = T::mfma32(qa, bf[ks], x);
+                for (int ks = 0; ks < D / 16; ++ks) {
+                    qa[ks] = as_frag<T>(lds_read128(aimg, S::off(l32, 2 * ks + hi)));
+                    if constexpr (C::KVL)
+                        kv[ks] = as_frag<T>(lds_read128(role_p ? kimg : smem + C::OFF_V,
+                                                        S::off(32 * kwave + l32, 2 * ks + hi)));
+                    else
+                        kv[ks] = bf[ks];
+                    // keep the reads ahead of the chain and in k-step order (counted waits)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int ks = 0; ks < D / 16; ++ks) x = T::mfma32(qa[ks], kv[ks], x);
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < D / 16; ++ks) {
+                    const auto qa = as_frag<T>(lds_read128(aimg, S::off(l32, 2 * ks + hi)));
+                    if constexpr (C::KVL)
+                        x = T::mfma32(qa, as_frag<T>(lds_read128(role_p ? kimg : smem + C::OFF_V,
+                                                                 S::off(32 * kwave + l32, 2 * ks + hi))), x);
+                    else
+                        x = T::mfma32(qa, bf[ks], x);
+                }
+            }
+            if (!FA_BWD_SPLIT_HOIST) {
+                const float *rcb = role_p ? lse_s + QB * C::BQ : del_s + QBD * C::BQ;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) rc4[g] = *reinterpret_cast<const f32x4 *>(rcb + 8 * g + 4 * hi);
+                if (!role_p) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) pw[j] = lds_read128(pxb, j * 1024 + lane * 16);
+                }
             }
             if (role_p) {
-                const float *lse_b = lse_s + QB * C::BQ;
-                const bool need_mask = (q0 + C::BQ > seqlen_q) || (k0 + C::BKV > seqlen_k) || (CAUSAL && q0 < kw + 31);
+                // P = exp2(S c - lse), the per-element mask in its own copy (taken on the causal
+                // diagonal and the ragged edges only)
+                auto pexp = [&](auto masked_tag) __attribute__((always_inline)) {
+                    constexpr bool MASKED = decltype(masked_tag)::value;
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x4 lse4 = *reinterpret_cast<const f32x4 *>(lse_b + 8 * g + 4 * hi);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int r = 4 * g + e;
-                        float p = fast_exp2(fmaf(x[r], c_log2, -lse4[e]));
-                        if (need_mask) {
+                    for (int r = 0; r < 16; ++r) {
+                        float p = fast_exp2(fmaf(x[r], c_log2, -rc4[r >> 2][r & 3]));
+                        if (MASKED) {
                             const int q = q0 + crow(r, hi);
                             if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
                         }
                         x[r] = p;
                     }
-                }
+                };
+                const bool need_mask = (q0 + C::BQ > seqlen_q) || (k0 + C::BKV > seqlen_k) || (CAUSAL && q0 < kw + 31);
+                if (FA_BWD_SPLIT_PROBE == 3)
+                    ;
+                else if (!FA_BWD_SPLIT_HOIST || __builtin_amdgcn_readfirstlane((int)need_mask))
+                    pexp(std::true_type{});
+                else
+                    pexp(std::false_type{});
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     lds_write128(pxb, j * 1024 + lane * 16,
                                  u32x4{__float_as_uint(x[4 * j]), __float_as_uint(x[4 * j + 1]),
                                        __float_as_uint(x[4 * j + 2]), __float_as_uint(x[4 * j + 3])});
             } else {
-                const float *del_b = del_s + QBD * C::BQ;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const u32x4 pw = lds_read128(pxb, j * 1024 + lane * 16);
-                    const f32x4 del4 = *reinterpret_cast<const f32x4 *>(del_b + 8 * j + 4 * hi);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) x[4 * j + e] = __uint_as_float(pw[e]) * (x[4 * j + e] - del4[e]);
+                    for (int e = 0; e < 4; ++e)
+                        x[4 * j + e] = FA_BWD_SPLIT_PROBE == 3 ? x[4 * j + e] + __uint_as_float(pw[j][e])
+                                                               : __uint_as_float(pw[j][e]) * (x[4 * j + e] - rc4[j][e]);
                 }
             }
             // dV^T += dO^T P (P waves) or dK^T += Q^T dS (dS waves), A operands by transposed reads
@@ -506,8 +568,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
             }
         }
         // tile u+1 into buffer (u+1)%3: it held tile u-2, last read by the dS waves in step u-1
-        if (u + 1 < nqt) lds_store_qtile((QB + 1) % 3);
-        __syncthreads();
+        if (u + 1 < nqt && FA_BWD_SPLIT_PROBE != 5) lds_store_qtile((QB + 1) % 3);
+        // timing probes (wrong results by design): FA_BWD_SPLIT_PROBE 1 = no barrier in odd steps,
+        // 2 = no barrier at all, 3 = no exp / dS VALU (P = S), 4 = no query-tile loads, 5 = no query-tile
+        // LDS stores
+        if (!(FA_BWD_SPLIT_PROBE == 2 || (FA_BWD_SPLIT_PROBE == 1 && (u & 1)))) __syncthreads();
     };
 
     if constexpr (C::SKEW) {

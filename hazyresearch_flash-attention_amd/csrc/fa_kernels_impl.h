@@ -94,8 +94,7 @@ static hipError_t launch_bwd_s(const FaBwdArgs &a, const FaBlockMask &bm, hipStr
     // the main kernel's atomics or by the query-major pass (bwd_dq_direct)
     if constexpr (D == 128) {
         constexpr bool DQK = bwd_dqk_tile(D) && !DROPOUT && !SPARSE;
-        using C = BwdSplitCfg<D, (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL,
-                              bwd_split_skew(!DQK, DROPOUT, SPARSE)>;
+        using C = BwdSplitCfgOf<D, CAUSAL, DROPOUT, SPARSE, !DQK>;
         auto kern = fa_bwd_split_kernel<D, T, CAUSAL, DROPOUT, SPARSE, !DQK>;
         FA_ENSURE_LDS(kern, C::LDS_BYTES);
         static const int slots = xcd_slots_of(kern, C::NT, C::LDS_BYTES);
