@@ -25,38 +25,48 @@ namespace fa {
 #define FA_BWD_SPLIT_KVL_NC 1   // 1: the non-causal ones too (D=128 non-causal 1.00 -> 0.95 ms)
 #endif
 
-template <int D, bool KVL_ = false, bool SKEW_ = false>
+template <int D, bool KVL_ = false, bool SKEW_ = false, int SUB_ = 1>
 struct BwdSplitCfg {
     // SKEW (dense, no dropout, dQ by the query-major pass): the P waves run one query tile ahead
     // of the dS waves, so Q/dO/lse/delta rotate through 3 buffers and P through 2
     static constexpr bool SKEW = SKEW_;
+    // SUB (skewed kernels): 32-row query sub-tiles per step. With 2, each wave runs two
+    // independent MFMA chains and twice the matrix work per barrier, and P crosses LDS as the
+    // 16-bit words of the dV operand (the fp32 exchange would not fit next to 64-row images)
+    static constexpr int SUB = SKEW ? SUB_ : 1;
+    static constexpr bool P16 = SUB > 1;
     static constexpr int NQB = SKEW ? 3 : 2;
     static constexpr int NPX = SKEW ? 2 : 1;
     static constexpr int NW = 8;            // waves per workgroup
     static constexpr int NT = 64 * NW;
     static constexpr int KEYW = NW / 2;     // wave pairs, 32 keys each
     static constexpr int BKV = 32 * KEYW;   // keys per workgroup
-    static constexpr int BQ = 32;
+    static constexpr int BQ = 32 * SUB;
     static constexpr int NC = D / 8;
+    // KVL (causal): K and V rows re-read from LDS images per query tile instead of 32 registers
+    static constexpr bool KVL = KVL_;
+    // the K image: the B operand of dQ (non-skewed kernels) and the KVL reads
+    static constexpr bool KIMG = !SKEW || KVL;
     static constexpr int K_IMG = BKV * D * 2;
     static constexpr int Q_IMG = BQ * D * 2;
     static constexpr int DS_IMG = BKV * BQ * 2;
     static constexpr int OFF_K = 0;
-    static constexpr int OFF_Q = OFF_K + K_IMG;          // Q[NQB]
+    static constexpr int OFF_Q = OFF_K + (KIMG ? K_IMG : 0);   // Q[NQB]
     static constexpr int OFF_DO = OFF_Q + NQB * Q_IMG;   // dO[NQB]
     static constexpr int OFF_DS = OFF_DO + NQB * Q_IMG;
     static constexpr int OFF_LSE = OFF_DS + (SKEW ? 0 : DS_IMG);   // lse[NQB][BQ]
     static constexpr int OFF_DELTA = OFF_LSE + NQB * BQ * 4;
     static constexpr int OFF_QLIVE = OFF_DELTA + NQB * BQ * 4;
     static constexpr int QLIVE_WORDS = 16;
-    // P exchange: per wave pair 4 chunks x 64 lanes x 16 B (chunk-major: conflict-free b128)
+    // P exchange: per wave pair and sub-tile, 4 (fp32) or 2 (16-bit) chunks x 64 lanes x 16 B
+    // (chunk-major: conflict-free b128)
     static constexpr int OFF_PX = OFF_QLIVE + QLIVE_WORDS * 8;
-    static constexpr int PX_PAIR = 4 * 64 * 16;
-    // KVL (causal): K and V rows re-read from LDS images per query tile instead of 32 registers
-    static constexpr bool KVL = KVL_;
+    static constexpr int PX_SUB = (P16 ? 2 : 4) * 64 * 16;
+    static constexpr int PX_PAIR = SUB * PX_SUB;
     static constexpr int OFF_V = OFF_PX + NPX * KEYW * PX_PAIR;
     static constexpr int LDS_BYTES = OFF_V + (KVL ? K_IMG : 0);
     static constexpr int QCH = (BQ * NC + NT - 1) / NT;
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
 #ifndef FA_BWD_SPLIT_KVL_SKEW
@@ -67,6 +77,9 @@ struct BwdSplitCfg {
 #endif
 #ifndef FA_BWD_SPLIT_HOIST
 #define FA_BWD_SPLIT_HOIST 1  // 1: skewed steps read their row constants and operands ahead, mask unswitched
+#endif
+#ifndef FA_BWD_SPLIT_SUB
+#define FA_BWD_SPLIT_SUB 1    // 32-row query sub-tiles per skewed step (2: C4 even, D=128 -2 %; needs the default scheduler)
 #endif
 #ifndef FA_BWD_SPLIT_SKEW
 #define FA_BWD_SPLIT_SKEW 1   // 1: P waves one query tile ahead of dS waves (dense, no dropout, no dQ)
@@ -81,7 +94,7 @@ using BwdSplitCfgOf = BwdSplitCfg<D,
                                   bwd_split_skew(DQ, DROPOUT, SPARSE)
                                       ? (bool)FA_BWD_SPLIT_KVL_SKEW
                                       : (CAUSAL || FA_BWD_SPLIT_KVL_NC) && FA_BWD_SPLIT_KVL,
-                                  bwd_split_skew(DQ, DROPOUT, SPARSE)>;
+                                  bwd_split_skew(DQ, DROPOUT, SPARSE), FA_BWD_SPLIT_SUB>;
 
 // DQ = false: no dS image and no dQ (fa_bwd_dq_kernel computes dQ query-major, no atomics)
 template <int D, typename T, bool CAUSAL, bool DROPOUT, bool SPARSE = false, bool DQ = true>
@@ -152,12 +165,12 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
     const int64_t dqa_row = (int64_t)a.nheads * head_dim;
 
     // ---- K block image (B operand of dQ = dS K)
-    for (int idx = tid; idx < C::BKV * C::NC; idx += C::NT) {
+    for (int idx = tid; (C::KIMG || C::KVL) && idx < C::BKV * C::NC; idx += C::NT) {
         const int row = idx / C::NC, c = idx % C::NC;
         const int kv = k0 + row;
         u32x4 v = {0u, 0u, 0u, 0u};
         if (kv < seqlen_k && c * 8 < head_dim) v = gload128(kp + (int64_t)kv * a.k_row_stride + c * 8);
-        lds_write128(kimg, S::off(row, c), v);
+        if constexpr (C::KIMG) lds_write128(kimg, S::off(row, c), v);
         if constexpr (C::KVL) {
             u32x4 w = {0u, 0u, 0u, 0u};
             if (kv < seqlen_k && c * 8 < head_dim) w = gload128(vp + (int64_t)kv * a.v_row_stride + c * 8);
@@ -575,16 +588,145 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
         if (!(FA_BWD_SPLIT_PROBE == 2 || (FA_BWD_SPLIT_PROBE == 1 && (u & 1)))) __syncthreads();
     };
 
+    // ---- skewed step over two 32-row sub-tiles (C::SUB == 2): as sstep, with both sub-tiles'
+    // chains interleaved (independent accumulators), a four-k-step window of operand reads, and P
+    // exchanged as the packed 16-bit words the P waves feed their own dV MFMAs
+    auto sstep2 = [&](auto qb_tag, int u) __attribute__((always_inline)) {
+        constexpr int QB = decltype(qb_tag)::value;           // buffer of tile u
+        // LDS bases past 64 KiB (beyond the 16-bit ds offset) tied to the step (u >> 30 is 0), so
+        // per-lane addresses are formed next to their reads, not hoisted as dozens of registers
+        const int zu = __builtin_amdgcn_readfirstlane(u >> 30);
+        auto step_base = [&](int off) __attribute__((always_inline)) { return off + zu; };
+        constexpr int QBD = (QB + 2) % 3;                      // buffer of tile u-1 (dS waves)
+        if (u + 1 < nqt) gload_qtile(q_begin + (u + 1) * C::BQ);
+        const int tile = role_p ? u : u - 1;
+        const int q0 = q_begin + tile * C::BQ;
+        const bool has = role_p ? u < nqt : u >= 1;
+        const bool active = has && (!CAUSAL || (q0 + C::BQ - 1 >= kw));
+        char *pxb = smem + step_base(C::OFF_PX + kwave * C::PX_PAIR + ((role_p ? u : u - 1) & 1) * (C::KEYW * C::PX_PAIR));
+        if (active) {
+            const int qbuf = role_p ? QB : QBD;
+            const char *qimg = smem + step_base(C::OFF_Q + qbuf * C::Q_IMG);
+            const char *doimg = smem + step_base(C::OFF_DO + qbuf * C::Q_IMG);
+            const char *aimg = role_p ? qimg : doimg;
+            constexpr int NKS = D / 16, WIN = 1;
+            f32x16 x[2];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { x[0][r] = 0.f; x[1][r] = 0.f; }
+            u32x4 qa[2][NKS];
+            auto rd = [&](int ks) __attribute__((always_inline)) {
+#pragma unroll
+                for (int sb = 0; sb < 2; ++sb) qa[sb][ks] = lds_read128(aimg, S::off(32 * sb + l32, 2 * ks + hi));
+            };
+#pragma unroll
+            for (int ks = 0; ks < WIN; ++ks) rd(ks);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const auto kf = C::KVL ? as_frag<T>(lds_read128(role_p ? kimg : smem + C::OFF_V,
+                                                                S::off(32 * kwave + l32, 2 * ks + hi)))
+                                       : bf[ks];
+                x[0] = T::mfma32(as_frag<T>(qa[0][ks]), kf, x[0]);
+                x[1] = T::mfma32(as_frag<T>(qa[1][ks]), kf, x[1]);
+                if (ks + WIN < NKS) rd(ks + WIN);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            u32x4 pk[2][2];   // [sub-tile][16-row half]: packed 16-bit P (P waves) or dS (dS waves)
+            if (role_p) {
+                const float *lse_b = (const float *)(smem + step_base(C::OFF_LSE + QB * C::BQ * 4));
+#pragma unroll
+                for (int sb = 0; sb < 2; ++sb) {
+                    const int q0s = q0 + 32 * sb;
+                    f32x4 rc4[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) rc4[g] = *reinterpret_cast<const f32x4 *>(lse_b + 32 * sb + 8 * g + 4 * hi);
+                    auto pexp = [&](auto masked_tag) __attribute__((always_inline)) {
+                        constexpr bool MASKED = decltype(masked_tag)::value;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            float p = fast_exp2(fmaf(x[sb][r], c_log2, -rc4[r >> 2][r & 3]));
+                            if (MASKED) {
+                                const int q = q0s + crow(r, hi);
+                                if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
+                            }
+                            x[sb][r] = p;
+                        }
+                    };
+                    const bool need_mask = (q0s + 32 > seqlen_q) || (k0 + C::BKV > seqlen_k) || (CAUSAL && q0s < kw + 31);
+                    if (__builtin_amdgcn_readfirstlane((int)need_mask))
+                        pexp(std::true_type{});
+                    else
+                        pexp(std::false_type{});
+#pragma unroll
+                    for (int sg = 0; sg < 2; ++sg) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) pk[sb][sg][e] = T::pack2(x[sb][8 * sg + 2 * e], x[sb][8 * sg + 2 * e + 1]);
+                        lds_write128(pxb, sb * C::PX_SUB + sg * 1024 + lane * 16, pk[sb][sg]);
+                    }
+                }
+            } else {
+                const float *del_b = (const float *)(smem + step_base(C::OFF_DELTA + QBD * C::BQ * 4));
+#pragma unroll
+                for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+                    for (int sg = 0; sg < 2; ++sg) {
+                        const u32x4 pw = lds_read128(pxb, sb * C::PX_SUB + sg * 1024 + lane * 16);
+                        const f32x4 dA = *reinterpret_cast<const f32x4 *>(del_b + 32 * sb + 16 * sg + 4 * hi);
+                        const f32x4 dB = *reinterpret_cast<const f32x4 *>(del_b + 32 * sb + 16 * sg + 8 + 4 * hi);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            // registers 8 sg + 2e, +1: rows crow(., hi) = 16 sg + (2e < 4 ? 0 : 8) + 4hi + (2e & 3), +1
+                            const int r = 8 * sg + 2 * e;
+                            const f32x4 &dl = (e < 2) ? dA : dB;
+                            const float p0 = T::lo_float(pw[e]), p1 = T::hi_float(pw[e]);
+                            const float s0 = p0 * (x[sb][r] - dl[(2 * e) & 3]);
+                            const float s1 = p1 * (x[sb][r + 1] - dl[(2 * e + 1) & 3]);
+                            pk[sb][sg][e] = T::pack2(s0, s1);
+                        }
+                    }
+                }
+            }
+            // dV^T += dO^T P (P waves) or dK^T += Q^T dS (dS waves), A operands by transposed reads
+            const char *timg = role_p ? doimg : qimg;
+#pragma unroll
+            for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+                for (int sg = 0; sg < 2; ++sg) {
+                    const int rb = 32 * sb + 16 * sg + 4 * hi + qq;
+#pragma unroll
+                    for (int dt = 0; dt < D / 32; ++dt) {
+                        const int col = 32 * dt + 16 * grp + 4 * pp;
+                        u32x2 a0 = lds_read_tr(timg, S::off8(rb, col));
+                        u32x2 a1 = lds_read_tr(timg, S::off8(rb + 8, col));
+                        acc[dt] = T::mfma32(as_frag<T>(u32x4{a0[0], a0[1], a1[0], a1[1]}), as_frag<T>(pk[sb][sg]), acc[dt]);
+                    }
+                }
+        }
+        // tile u+1 into buffer (u+1)%3: it held tile u-2, last read by the dS waves in step u-1
+        if (u + 1 < nqt) lds_store_qtile((QB + 1) % 3);
+        __syncthreads();
+    };
+
     if constexpr (C::SKEW) {
         // the prologue stored tile 0 in buffer 0; steps u = 0 .. nqt (the last one: dS waves only)
         int u = 0;
-        for (; u + 2 <= nqt; u += 3) {
-            sstep(std::integral_constant<int, 0>(), u);
-            sstep(std::integral_constant<int, 1>(), u + 1);
-            sstep(std::integral_constant<int, 2>(), u + 2);
+        if constexpr (C::SUB == 2) {
+            for (; u + 2 <= nqt; u += 3) {
+                sstep2(std::integral_constant<int, 0>(), u);
+                sstep2(std::integral_constant<int, 1>(), u + 1);
+                sstep2(std::integral_constant<int, 2>(), u + 2);
+            }
+            if (u <= nqt) sstep2(std::integral_constant<int, 0>(), u++);
+            if (u <= nqt) sstep2(std::integral_constant<int, 1>(), u++);
+        } else {
+            for (; u + 2 <= nqt; u += 3) {
+                sstep(std::integral_constant<int, 0>(), u);
+                sstep(std::integral_constant<int, 1>(), u + 1);
+                sstep(std::integral_constant<int, 2>(), u + 2);
+            }
+            if (u <= nqt) sstep(std::integral_constant<int, 0>(), u++);
+            if (u <= nqt) sstep(std::integral_constant<int, 1>(), u++);
         }
-        if (u <= nqt) sstep(std::integral_constant<int, 0>(), u++);
-        if (u <= nqt) sstep(std::integral_constant<int, 1>(), u++);
     } else if constexpr (SPARSE) {
         int it = t_first;
         while (it < nqt) {

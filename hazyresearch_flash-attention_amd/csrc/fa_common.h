@@ -43,6 +43,9 @@ struct Bf16 {
         bf16x2 v = {(__bf16)a, (__bf16)b};
         return __builtin_bit_cast(uint32_t, v);
     }
+    // the two halves of a pack2 word back to fp32 (exact)
+    static __device__ __forceinline__ float lo_float(uint32_t w) { return __uint_as_float(w << 16); }
+    static __device__ __forceinline__ float hi_float(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
     static __device__ __forceinline__ f32x16 mfma32(frag a, frag b, f32x16 c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
     }
@@ -65,6 +68,8 @@ struct Fp16 {
         f16x2 v = {(_Float16)a, (_Float16)b};
         return __builtin_bit_cast(uint32_t, v);
     }
+    static __device__ __forceinline__ float lo_float(uint32_t w) { return to_float((uint16_t)(w & 0xFFFFu)); }
+    static __device__ __forceinline__ float hi_float(uint32_t w) { return to_float((uint16_t)(w >> 16)); }
     static __device__ __forceinline__ f32x16 mfma32(frag a, frag b, f32x16 c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
     }
