@@ -38,6 +38,11 @@ namespace fa {
 #ifndef FA_BWD_RC_ALL
 #define FA_BWD_RC_ALL 0         // 1: every lane of the staging half stages the row constants (no lane branch)
 #endif
+// timing probes (wrong results by design, A/B builds only): 1 = no barrier per
+// query tile, 2 = no dQ phase, 3 = no P / dS VALU
+#ifndef FA_BWD_PROBE
+#define FA_BWD_PROBE 0
+#endif
 #ifndef FA_BWD_HOIST
 #define FA_BWD_HOIST 1   // 1: S / dZ operands read ahead of their MFMA chains (D = 64, dense)
 #endif
@@ -587,7 +592,9 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                     }
                 }
             };
-            if (__builtin_amdgcn_readfirstlane((int)need_mask))
+            if (FA_BWD_PROBE == 3)
+                ;
+            else if (__builtin_amdgcn_readfirstlane((int)need_mask))
                 pds(std::true_type{});
             else
                 pds(std::false_type{});
@@ -616,14 +623,14 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             // dQ runs one tile behind: the previous tile's dS image is complete since the barrier
             // that closed the previous step, so each step needs a single barrier (the dS image of
             // this tile is read in the next step, the other buffer)
-            if (itp >= 0) {
+            if (itp >= 0 && FA_BWD_PROBE != 2) {
                 dq_phase(dsimg + (1 - BUF) * C::DS_IMG, q_begin + itp * C::BQ, store_buf, q_begin + itn * C::BQ);
                 stored = true;
             }
         }
         // waves without a dQ tile (or steps without a dQ phase) store the staged tile here
         if (store_buf >= 0 && !(stored && wave < 2 * (D / 16))) lds_store_qtile(store_buf, q_begin + itn * C::BQ);
-        __syncthreads();
+        if (FA_BWD_PROBE != 1) __syncthreads();
     };
     int ilast = -1, blast = 0;   // last tile and its buffer (its dQ runs after the walk)
     if constexpr (SPARSE) {
