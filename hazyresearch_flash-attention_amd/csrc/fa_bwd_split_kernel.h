@@ -459,9 +459,23 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
     // dV) while the dS waves take tile u-1 (dZ, dS from P image (u-1)&1, dK). Neither waits for the
     // other inside a step, so on each SIMD the P wave's exp work runs beside the dS wave's MFMAs and
     // the other way round; one barrier per step. Tile u+1 is prefetched into Q/dO buffer (u+1)%3.
+    // FA_BWD_SPLIT_PROBE == 6 (timing probe, wrong dK / dV by design): shader-clock stamps per
+    // step phase, summed over the steps and written over the first key row of each wave's output
+    uint64_t ph[5] = {0, 0, 0, 0, 0};
+    uint64_t tstamp = 0;
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if constexpr (FA_BWD_SPLIT_PROBE == 6) {
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+            if (i >= 0) ph[i] += t - tstamp;
+            tstamp = t;
+        }
+    };
     auto sstep = [&](auto qb_tag, int u) __attribute__((always_inline)) {
         constexpr int QB = decltype(qb_tag)::value;           // buffer of tile u
         constexpr int QBD = (QB + 2) % 3;                      // buffer of tile u-1 (dS waves)
+        stamp(-1);
         if (u + 1 < nqt && FA_BWD_SPLIT_PROBE != 4) gload_qtile(q_begin + (u + 1) * C::BQ);
         const int tile = role_p ? u : u - 1;
         const int q0 = q_begin + tile * C::BQ;
@@ -527,6 +541,12 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
                     for (int j = 0; j < 4; ++j) pw[j] = lds_read128(pxb, j * 1024 + lane * 16);
                 }
             }
+            if constexpr (FA_BWD_SPLIT_PROBE == 6) {
+                // the chain's result consumed before the stamp
+                float z = x[0] + x[15];
+                asm volatile("" :: "v"(z));
+            }
+            stamp(0);
             if (role_p) {
                 // P = exp2(S c - lse), the per-element mask in its own copy (taken on the causal
                 // diagonal and the ragged edges only)
@@ -563,6 +583,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
                                                                : __uint_as_float(pw[j][e]) * (x[4 * j + e] - rc4[j][e]);
                 }
             }
+            stamp(1);
             // dV^T += dO^T P (P waves) or dK^T += Q^T dS (dS waves), A operands by transposed reads
             const char *timg = role_p ? doimg : qimg;
 #pragma unroll
@@ -580,12 +601,19 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
                 }
             }
         }
+        if constexpr (FA_BWD_SPLIT_PROBE == 6) {
+            float z = acc[0][0] + acc[D / 32 - 1][15];
+            asm volatile("" :: "v"(z));
+        }
+        stamp(2);
         // tile u+1 into buffer (u+1)%3: it held tile u-2, last read by the dS waves in step u-1
         if (u + 1 < nqt && FA_BWD_SPLIT_PROBE != 5) lds_store_qtile((QB + 1) % 3);
+        stamp(3);
         // timing probes (wrong results by design): FA_BWD_SPLIT_PROBE 1 = no barrier in odd steps,
         // 2 = no barrier at all, 3 = no exp / dS VALU (P = S), 4 = no query-tile loads, 5 = no query-tile
         // LDS stores
         if (!(FA_BWD_SPLIT_PROBE == 2 || (FA_BWD_SPLIT_PROBE == 1 && (u & 1)))) __syncthreads();
+        stamp(4);
     };
 
     // ---- skewed step over two 32-row sub-tiles (C::SUB == 2): as sstep, with both sub-tiles'
@@ -745,6 +773,18 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
         }
     }
 
+    if constexpr (FA_BWD_SPLIT_PROBE == 6) {
+        // phases: 0 = operand reads + S / dZ chain, 1 = P / dS VALU (+ P exchange), 2 = update
+        // MFMAs (transposed reads, results consumed), 3 = staging LDS stores, 4 = barrier; 5th word:
+        // the step count
+        if (lane == 0 && kw < seqlen_k) {
+            uint64_t *o = (uint64_t *)(role_p ? (uint16_t *)a.dv + (int64_t)(k_start + kw) * a.dv_row_stride + (int64_t)h * a.dv_head_stride
+                                              : (uint16_t *)a.dk + (int64_t)(k_start + kw) * a.dk_row_stride + (int64_t)h * a.dk_head_stride);
+            for (int i = 0; i < 5; ++i) o[i] = ph[i];
+            o[5] = (uint64_t)(nqt + 1);
+        }
+        return;
+    }
     // ---- epilogue: dV (P waves) or scaled dK (dS waves) rows of this lane's key
     if (kvrow < seqlen_k) {
         uint16_t *outp = role_p
