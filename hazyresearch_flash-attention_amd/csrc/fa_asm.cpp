@@ -87,6 +87,9 @@ static_assert(offsetof(FaAsmFwdArgs, q_rs) == 88 && offsetof(FaAsmFwdArgs, c) ==
 namespace {
 
 constexpr int kRows = 256;            // query rows per workgroup
+#ifndef FA_ASM_GROUP_WGS
+#define FA_ASM_GROUP_WGS 64          // causal D > 64: workgroups per XCD head group (2x the 32 a XCD runs)
+#endif
 constexpr int kMaxDev = 64;
 constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
 
@@ -300,7 +303,7 @@ hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavaila
     if (a.is_causal && k.nbh % 8 == 0 && a.head_dim > 64) {
         // G nqb ~ 2x the workgroups one XCD runs at once (one per CU: 32), G dividing the XCD's
         // nbh / 8 heads so that every group is full (the HIP kernels' measured choice, x2 slots)
-        const uint32_t nh = k.nbh / 8, want = (64 + nqb - 1) / nqb;
+        const uint32_t nh = k.nbh / 8, want = (FA_ASM_GROUP_WGS + nqb - 1) / nqb;
         uint32_t g = 1;
         for (uint32_t c = 1; c <= nh && c <= want; ++c)
             if (nh % c == 0) g = c;
