@@ -43,6 +43,9 @@ namespace fa {
 #ifndef FA_BWD_PROBE
 #define FA_BWD_PROBE 0
 #endif
+#ifndef FA_BWD_ROT_WALK
+#define FA_BWD_ROT_WALK 1   // non-causal: query-tile walk rotated per key block (see qrow)
+#endif
 #ifndef FA_BWD_HOIST
 #define FA_BWD_HOIST 1   // 1: S / dZ operands read ahead of their MFMA chains (D = 64, dense)
 #endif
@@ -283,6 +286,21 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
 
     const int q_begin = CAUSAL ? k0 : 0;   // rows q < k0 see no key of this block
     const int nqt = seqlen_q > q_begin ? (seqlen_q - q_begin + C::BQ - 1) / C::BQ : 0;
+    // Non-causal dense kernels walk the query tiles from a per-key-block offset (tile (t + rot) % nqt
+    // at step t): the key blocks of one head run at the same time on one XCD, and walking in lockstep
+    // from tile 0 they added their dQ partials into the same rows at the same moment (same-address
+    // atomics serialise in the L2). Causal blocks start at their own diagonal already.
+    constexpr bool ROT = FA_BWD_ROT_WALK && !CAUSAL && !SPARSE && DQ;
+    const int rot = ROT && nqt > 0 ? (int)(((int64_t)(k0 / C::BKV) * nqt) / ((seqlen_k + C::BKV - 1) / C::BKV)) % nqt : 0;
+    auto qrow = [&](int t) __attribute__((always_inline)) -> int {
+        if constexpr (!ROT) {
+            return q_begin + t * C::BQ;
+        } else {
+            int u = t + rot;
+            u -= u >= nqt ? nqt : 0;
+            return q_begin + u * C::BQ;
+        }
+    };
 
     // ---- query-tile staging (T14): a tile is loaded into registers two steps before its use and
     // written to its LDS image one step before. The two halves of the workgroup take turns: half
@@ -377,10 +395,10 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
     const int t_second = t_first < nqt ? next_qt(t_first) : nqt;
     if (t_first < nqt) {
         if (stg_half == 0) {
-            gload_qtile(q_begin + t_first * C::BQ);
-            lds_store_qtile(0, q_begin + t_first * C::BQ);
+            gload_qtile(qrow(t_first));
+            lds_store_qtile(0, qrow(t_first));
         } else if (t_second < nqt) {
-            gload_qtile(q_begin + t_second * C::BQ);
+            gload_qtile(qrow(t_second));
         }
     }
     __syncthreads();
@@ -457,9 +475,9 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         char *doimg = smem + C::OFF_DO + BUF * C::Q_IMG;
         const float *lse_b = lse_s + BUF * C::BQ;
         const float *del_b = del_s + BUF * C::BQ;
-        const int q0 = q_begin + it * C::BQ;
+        const int q0 = qrow(it);
         char *dsw = dsimg + BUF * C::DS_IMG;
-        if (my_load && itnn < nqt) gload_qtile(q_begin + itnn * C::BQ);
+        if (my_load && itnn < nqt) gload_qtile(qrow(itnn));
         // (block sparsity: a dead 16-row half of a live tile has lse = +inf in its row constants)
         const bool active = !CAUSAL || (q0 + C::BQ - 1 >= kw);
         u32x4 pk[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}}, sk[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
@@ -624,12 +642,12 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
             // that closed the previous step, so each step needs a single barrier (the dS image of
             // this tile is read in the next step, the other buffer)
             if (itp >= 0 && FA_BWD_PROBE != 2) {
-                dq_phase(dsimg + (1 - BUF) * C::DS_IMG, q_begin + itp * C::BQ, store_buf, q_begin + itn * C::BQ);
+                dq_phase(dsimg + (1 - BUF) * C::DS_IMG, qrow(itp), store_buf, qrow(itn));
                 stored = true;
             }
         }
         // waves without a dQ tile (or steps without a dQ phase) store the staged tile here
-        if (store_buf >= 0 && !(stored && wave < 2 * (D / 16))) lds_store_qtile(store_buf, q_begin + itn * C::BQ);
+        if (store_buf >= 0 && !(stored && wave < 2 * (D / 16))) lds_store_qtile(store_buf, qrow(itn));
         if (FA_BWD_PROBE != 1) __syncthreads();
     };
     int ilast = -1, blast = 0;   // last tile and its buffer (its dQ runs after the walk)
@@ -662,9 +680,9 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
         // dQ of the last tile (its dS image is complete since the last step's closing barrier)
         if (ilast >= 0) {
             if (blast)
-                dq_phase(dsimg + C::DS_IMG, q_begin + ilast * C::BQ, -1, 0);
+                dq_phase(dsimg + C::DS_IMG, qrow(ilast), -1, 0);
             else
-                dq_phase(dsimg, q_begin + ilast * C::BQ, -1, 0);
+                dq_phase(dsimg, qrow(ilast), -1, 0);
         }
     }
 
