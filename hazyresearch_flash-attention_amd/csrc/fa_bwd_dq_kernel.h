@@ -19,6 +19,13 @@
 
 namespace fa {
 
+#ifndef FA_BWD_DQ_SEED
+#define FA_BWD_DQ_SEED 1       // dP^T accumulator seeded with -delta
+#endif
+#ifndef FA_BWD_DQ_UNSWITCH
+#define FA_BWD_DQ_UNSWITCH 1   // per-element mask only on the tiles that need it (uniform branch)
+#endif
+
 
 template <int D, int NW>
 struct DqCfg {
@@ -172,33 +179,44 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a
         if (j + 1 < nt) gload_kv(j + 1);
         const bool need_mask = (kv0 + C::BN > seqlen_k) || (CAUSAL && kv0 + C::BN - 1 > qw);
         typename T::frag pf[2][2];
+        // dP^T's accumulator starts at -delta (the lane's row constant), so dS = P dP is one
+        // multiply per element; the per-element key/causal mask runs only on the tiles that need it,
+        // as a second copy of the sub-tile behind one wave-uniform branch (with the test inside the
+        // element loop the compiler computed the mask's compares and selects on every tile)
+        auto sub_tiles = [&](auto masked_tag) __attribute__((always_inline)) {
+            constexpr bool MASKED = decltype(masked_tag)::value;
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            f32x16 s, dp;
+            for (int st = 0; st < 2; ++st) {
+                f32x16 s, dp;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+                for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = FA_BWD_DQ_SEED ? -delta : 0.f; }
 #pragma unroll
-            for (int ks = 0; ks < D / 16; ++ks) {
-                s = T::mfma32(as_frag<T>(lds_read128(kb, k_rd[st][ks])), qf[ks], s);
-                dp = T::mfma32(as_frag<T>(lds_read128(vb, k_rd[st][ks])), df[ks], dp);
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float p = fast_exp2(fmaf(s[r], c_log2, -lse2));
-                if (need_mask) {
-                    const int kv = kv0 + 32 * st + crow(r, hi);
-                    if (kv >= seqlen_k || (CAUSAL && kv > qrow)) p = 0.f;
+                for (int ks = 0; ks < D / 16; ++ks) {
+                    s = T::mfma32(as_frag<T>(lds_read128(kb, k_rd[st][ks])), qf[ks], s);
+                    dp = T::mfma32(as_frag<T>(lds_read128(vb, k_rd[st][ks])), df[ks], dp);
                 }
-                s[r] = p * (dp[r] - delta);
-            }
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                u32x4 pk;
+                for (int r = 0; r < 16; ++r) {
+                    float p = fast_exp2(fmaf(s[r], c_log2, -lse2));
+                    if constexpr (MASKED) {
+                        const int kv = kv0 + 32 * st + crow(r, hi);
+                        if (kv >= seqlen_k || (CAUSAL && kv > qrow)) p = 0.f;
+                    }
+                    s[r] = FA_BWD_DQ_SEED ? p * dp[r] : p * (dp[r] - delta);
+                }
 #pragma unroll
-                for (int e = 0; e < 4; ++e) pk[e] = T::pack2(s[8 * s2 + 2 * e], s[8 * s2 + 2 * e + 1]);
-                pf[st][s2] = as_frag<T>(pk);
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    u32x4 pk;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) pk[e] = T::pack2(s[8 * s2 + 2 * e], s[8 * s2 + 2 * e + 1]);
+                    pf[st][s2] = as_frag<T>(pk);
+                }
             }
-        }
+        };
+        if (!FA_BWD_DQ_UNSWITCH || __builtin_amdgcn_readfirstlane((int)need_mask))
+            sub_tiles(std::true_type{});
+        else
+            sub_tiles(std::false_type{});
         // dQ^T += K^T dS^T
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt)
