@@ -200,7 +200,7 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a
                     float p = fast_exp2(fmaf(s[r], c_log2, -lse2));
                     if constexpr (MASKED) {
                         const int kv = kv0 + 32 * st + crow(r, hi);
-                        if (kv >= seqlen_k || (CAUSAL && kv > qrow)) p = 0.f;
+                        p = mask_min(p, kv >= seqlen_k || (CAUSAL && kv > qrow));
                     }
                     s[r] = FA_BWD_DQ_SEED ? p * dp[r] : p * (dp[r] - delta);
                 }

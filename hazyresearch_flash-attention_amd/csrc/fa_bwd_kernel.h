@@ -591,9 +591,7 @@ __global__ FA_BWD_BOUNDS(CAUSAL) void fa_bwd_kernel(const FaBwdArgs a, const FaB
                     for (int e = 0; e < 4; ++e) {
                         const int r = 4 * g + e;
                         float p = fast_exp2(fmaf(sacc[r], c_log2, -lse4[e]));
-                        if constexpr (MASKED) {
-                            if (kvrow >= seqlen_k || (CAUSAL && kvrow > q0 + crow(r, hi))) p = 0.f;
-                        }
+                        if constexpr (MASKED) p = mask_min(p, kvrow >= seqlen_k || (CAUSAL && kvrow > q0 + crow(r, hi)));
                         float dpv = zacc[r];
                         float pdv = p;
                         if (DROPOUT) {

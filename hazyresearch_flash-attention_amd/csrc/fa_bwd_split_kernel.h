@@ -557,7 +557,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
                         float p = fast_exp2(fmaf(x[r], c_log2, -rc4[r >> 2][r & 3]));
                         if (MASKED) {
                             const int q = q0 + crow(r, hi);
-                            if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
+                            p = mask_min(p, q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q));
                         }
                         x[r] = p;
                     }
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_split_kernel(const FaBwdArgs a,
                             float p = fast_exp2(fmaf(x[sb][r], c_log2, -rc4[r >> 2][r & 3]));
                             if (MASKED) {
                                 const int q = q0s + crow(r, hi);
-                                if (q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q)) p = 0.f;
+                                p = mask_min(p, q >= seqlen_q || kvrow >= seqlen_k || (CAUSAL && kvrow > q));
                             }
                             x[sb][r] = p;
                         }

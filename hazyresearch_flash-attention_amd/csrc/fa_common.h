@@ -86,6 +86,10 @@ __device__ __forceinline__ typename T::frag as_frag(u32x4 v) {
 __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// p (an exp2 result, >= 0) forced to 0 where `masked`: min(p, masked ? 0 : inf). Written as a
+// select of `p` itself, the compiler sank the exp into the unmasked arm and gave every element
+// its own divergent branch; the min keeps the exp on both arms, so the mask stays two VALU ops.
+__device__ __forceinline__ float mask_min(float p, bool masked) { return fminf(p, masked ? 0.f : INFINITY); }
 
 // XCD-aware work order. The dispatcher hands workgroup L (linear id) to XCD L & 7, and each XCD
 // takes its share in order of L >> 3; this maps L to a position Lp such that every XCD covers a
