@@ -22,6 +22,9 @@ namespace fa {
 #ifndef FA_BWD_DQ_SEED
 #define FA_BWD_DQ_SEED 1       // dP^T accumulator seeded with -delta
 #endif
+#ifndef FA_BWD_DQ_ENTRY_WAIT
+#define FA_BWD_DQ_ENTRY_WAIT 1 // vmcnt(0) the compiler sees before the key walk
+#endif
 #ifndef FA_BWD_DQ_UNSWITCH
 #define FA_BWD_DQ_UNSWITCH 1   // per-element mask only on the tiles that need it (uniform branch)
 #endif
@@ -236,6 +239,11 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_kernel(const FaBwdArgs a
         lds_store_kv(smem, smem + 2 * C::TILE_BYTES);
         __syncthreads();
     }
+    // Every prologue load (the Q / dO operands, lse, delta) is done before the walk, in a form the
+    // compiler's wait counters see: otherwise the loop header inherits them as pending from the
+    // entry edge, and every step's S / dP chain waited with vmcnt(7..1) for that step's own K/V
+    // prefetch loads (issued at its top, needed only at its end)
+    if (FA_BWD_DQ_ENTRY_WAIT) vmcnt0();
     for (int j = 0; j < nt; j += 2) {
         step(std::integral_constant<int, 0>(), j);
         if (j + 1 < nt) step(std::integral_constant<int, 1>(), j + 1);
