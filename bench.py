@@ -12,9 +12,9 @@ collective); value = total FLOPs of all ranks / max time.
 
 Rank 0 prints ONE JSON line. `roofline` is the forward kernel: algorithmic FLOPs per launch
 (4*B*H*S*S*D) / its average duration from HIP events around each launch on the launch stream.
-`cpu_baseline` times the oracle's naive fp32 attention (restating benchmarks/
-benchmark_flash_attention.py:14-36 / tests/test_flash_attn.py:115-159) on the host cores on a
-bounded sample (2 of the 8 sequences). `extra` carries the other BASELINE.json configs.
+`cpu_baseline` times the reference benchmark's naive attention (oracle.attention_pytorch_bench,
+restating benchmarks/benchmark_flash_attention.py:14-36, fp32 compute) on the host cores with
+torch.utils.benchmark.Timer, on a bounded sample (2 of the 8 sequences, ~10 s). `extra` carries the other BASELINE.json configs.
 """
 import argparse
 import json
@@ -106,25 +106,32 @@ def graph_ms(fn, n):
         return None
 
 
-def cpu_baseline(B, H, S, D):
-    """Oracle naive attention (fp32) on the host cores, bounded sample: 2 sequences."""
-    from oracle.attention_ref import attention_ref
+def cpu_baseline(B, H, S, D, min_s=10.0):
+    """The reference benchmark's naive PyTorch attention (benchmarks/benchmark_flash_attention.py:14-36,
+    restated as oracle.attention_pytorch_bench; fp32 compute through its upcast flag, no mask, no
+    dropout: the headline workload) timed on the host cores with torch.utils.benchmark.Timer.timeit,
+    as benchmarks/utils.py:8-20 benchmark_forward does, on a bounded sample: 2 of the 8 sequences,
+    enough calls for about `min_s` seconds."""
+    import torch.utils.benchmark as benchmark
+    from oracle.attention_ref import attention_pytorch_bench
     nb = 2
     g = torch.Generator().manual_seed(0)
-    q, k, v = (torch.randn(nb, S, H, D, generator=g).bfloat16() for _ in range(3))
-    attention_ref(q[:1, :256], k[:1, :256], v[:1, :256])  # warm
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        attention_ref(q, k, v)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el > 8.0 or reps >= 5:
-            break
-    flops = fwd_flops(nb, H, S, S, D, False) * reps
-    return {"value": round(flops / el / 1e12, 4), "unit": "TFLOPS", "cores": torch.get_num_threads(),
+    qkv = torch.randn(nb, S, 3, H, D, generator=g).bfloat16()
+    attention_pytorch_bench(qkv, None, 0.0, upcast=True)          # warm
+    t1 = time.perf_counter()
+    attention_pytorch_bench(qkv, None, 0.0, upcast=True)          # size the run
+    t1 = time.perf_counter() - t1
+    reps = max(3, min(200, math.ceil(min_s / max(t1, 1e-3))))
+    t = benchmark.Timer(stmt="fn(qkv, None, 0.0, upcast=True)",
+                        globals={"fn": attention_pytorch_bench, "qkv": qkv},
+                        num_threads=torch.get_num_threads())
+    m = t.timeit(reps)
+    flops = fwd_flops(nb, H, S, S, D, False)
+    return {"value": round(flops / m.mean / 1e12, 4), "unit": "TFLOPS", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"oracle attention_ref fp32 (upcast) on {nb} of {B} sequences (B={nb},H={H},S={S},D={D}), "
-                      f"{reps} reps, {el:.2f}s"}
+            "sample": f"benchmarks/benchmark_flash_attention.py:14-36 attention_ref (fp32 upcast, no mask, p=0) "
+                      f"on {nb} of {B} sequences (B={nb},H={H},S={S},D={D}), torch.utils.benchmark.Timer "
+                      f"timeit({reps}): {m.mean * 1e3:.1f} ms per call"}
 
 
 def read_traffic():

@@ -23,6 +23,12 @@ BUILD = os.environ.get("FA_BUILD_DIR", os.path.join(HERE, "build"))
 DEFAULT_OUT = os.path.join(HERE, "flash_attn", "libfa_hip.so")
 OUT = os.environ.get("FA_BUILD_OUT", DEFAULT_OUT)
 EXTRA_CFLAGS = os.environ.get("FA_EXTRA_CFLAGS", "").split()
+# backward timing probes compute wrong gradients: they need an explicit probe build, and never
+# into the product library's path
+_PROBE_FLAGS = [f for f in EXTRA_CFLAGS if "PROBE" in f and not f.endswith("PROBE=0")]
+if _PROBE_FLAGS and ("-DFA_AB_PROBE_BUILD" not in EXTRA_CFLAGS or OUT == DEFAULT_OUT):
+    raise SystemExit(f"build.py: {' '.join(_PROBE_FLAGS)} is a timing probe (wrong results by design): "
+                     "build it only with -DFA_AB_PROBE_BUILD and FA_BUILD_OUT set to a variant library")
 
 KERNEL_TUS = ["fa_d32_fwd.hip", "fa_d64_fwd.hip", "fa_d128_fwd.hip", "fa_d32_bwd.hip", "fa_d64_bwd.hip", "fa_d128_bwd.hip"]
 SOURCES = ["fa_api.cpp", "fa_asm.cpp", "fa_aux.hip", "fa_padding.hip", "fa_rotary.hip"] + KERNEL_TUS

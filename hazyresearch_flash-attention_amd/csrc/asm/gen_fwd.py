@@ -140,6 +140,8 @@ PRIO4 = False          # 8 waves: s_setprio 1 for waves 4-7 (the SIMD partners d
 STAGGER = False        # 8 waves: waves 4-7 run half a tile behind (their barrier mid-tile; ring 6)
 FIRST_MAX_W8 = False   # 8 waves: FIRST_MAX (tile 0's row max sets the starting shift) as in the 4-wave form
 STAGGER_FRAC = 0.5     # STAGGER: the group-1 barrier after this fraction of a phase's MFMAs
+PINGPONG = False       # 8 waves (with STAGGER, ring 6): each phase = its MFMAs, then the softmax; the
+#                        group-1 barrier between the two, so SIMD partners alternate matrix / vector work
 
 
 def rq(base):
@@ -959,6 +961,20 @@ class Gen:
         br = sm[-1] if sm and sm[-1].kind == 'br' else None
         body = sm[:-1] if br else sm
         n = len(body)
+        if PINGPONG:
+            # matrix segment: the MFMAs with the DMA pieces and the K(t+2) reads (behind QK(t+1))
+            # in their gaps; vector segment: the softmax with the V^T(t) reads spread over it (every
+            # P.V MFMA that read V^T(t-1) is issued by then). Waves 4-7 take their barrier between
+            # the two segments (tile_body), so each SIMD pairs one wave's MFMAs with its partner's
+            # softmax.
+            for x in vr:
+                x.not_before = None
+            vseg = merge(body, [(i, x) for i, x in zip(spread(len(vr), 2, max(3, n - 8)), vr)])
+            if br:
+                vseg.append(br)
+            if vseg:
+                vseg[0].not_before = len(mf)
+            return [mark()] + place(mf, dma + kr + vseg)
         k_lo = n * len(qk) // max(1, len(mf)) + 1
         fill = merge(body, [(i, x) for i, x in zip(spread(len(kr), k_lo, n * 3 // 4), kr)] +
                      [(i, x) for i, x in zip(spread(len(dma), 4, n // 2), dma)])
@@ -1904,6 +1920,7 @@ def dump_block(regs):
 
 
 DUMP = None   # (point, [registers]) set by --dump
+LOOP_BLOCKS = set()   # ids of the main-loop and masked-loop tile blocks (the nolgkm / novm probes' scope)
 
 # 'stamps' probe (tools/asm_wg_timeline.py, D = 64 only): s_memrealtime (100 MHz) at kernel entry
 # (v168:169), after the prologue's first barrier (v180:181), at the last tile's entry (v170:171)
@@ -2025,6 +2042,13 @@ def stagger_split(lst):
     mf = [i for i, x in enumerate(lst) if x.kind == 'mfma']
     k = max(1, min(len(mf) - 1, round(len(mf) * STAGGER_FRAC)))
     cut = mf[k - 1] + 1
+    if PINGPONG:
+        # between the matrix and the vector segment: after the last MFMA and the fillers placed
+        # in its gap that are not softmax (DMA, K reads, SALU)
+        cut = mf[-1] + 1
+        while cut < len(lst) and lst[cut].kind in ('dma', 'm0', 'salu', 'ds') and lst[cut].txt.startswith(
+                ('buffer_load', 's_add_u32 m0', 's_add', 's_sub', 's_addc', 's_cselect', 'ds_read_b128')):
+            cut += 1
     return lst[:cut], lst[cut:], sum(1 for x in lst[:cut] if x.kind == 'dma')
 
 
@@ -2133,6 +2157,8 @@ def build(g):
             blk.append(raw('s_branch .Lloop'))
         tiles.append(blk)
     masks = [masked_tile(g, t, rescue) for t in range(U)]
+    LOOP_BLOCKS.clear()
+    LOOP_BLOCKS.update(id(b) for b in tiles + masks)
     lasts = [last_tile(g, t, rescue) for t in range(U)]
     lastsu = [last_tile(g, t, rescue, masked=False) for t in range(U)] if LAST_UNMASKED else []
     tiles1, masks1, lasts1, lastsu1 = [], [], [], []
@@ -2261,7 +2287,14 @@ def build(g):
 def emit(g, blocks):
     name = g.name
     if 'nolgkm' in PROBE or 'novm' in PROBE:
-        for blk in blocks[1:]:
+        # timing probes: the counted waits of the main-loop tiles only (never the prologue's, which
+        # cover the scalar loads of kernel arguments and cu_seqlens: without them the descriptors
+        # are built from stale SGPRs and the kernel faults -- a persistent-form probe run of round 6
+        # did exactly that when this stripped every block but the first)
+        for blk in blocks:
+            if id(blk) not in LOOP_BLOCKS:
+                continue
+            assert not any(x.kind == 'smem' for x in blk)
             blk[:] = [x for x in blk if not (x.txt.startswith('s_waitcnt') and
                                              (('nolgkm' in PROBE and 'lgkmcnt' in x.txt) or
                                               ('novm' in PROBE and 'vmcnt' in x.txt and 'lgkm' not in x.txt)))]
@@ -2334,6 +2367,7 @@ def main():
     ap.add_argument('--stagger', type=int, default=0, help='8 waves: waves 4-7 half a tile behind (ring 6)')
     ap.add_argument('--fmax8', type=int, default=0, help="8 waves: tile 0's row max sets the starting shift")
     ap.add_argument('--sfrac', type=float, default=None, help='STAGGER: group-1 barrier after this fraction of the MFMAs')
+    ap.add_argument('--pingpong', type=int, default=0, help='8 waves: matrix / vector segments alternating between SIMD partners')
     ap.add_argument('--lag8', default=None, help='8 waves: EXP_LAG,CVT_LAG')
     ap.add_argument('--persist', type=int, default=0, help='persistent workgroups: next-block K/V tail (and next-Q prefetch at D = 64), 4 waves')
     ap.add_argument('--out', required=True)
@@ -2436,6 +2470,10 @@ def main():
         STAGGER_FRAC = args.sfrac
     if args.lag8 and NWAVES == 8:
         EXP_LAG, CVT_LAG = (int(x) for x in args.lag8.split(','))
+        set_geometry(6, 3)
+    global PINGPONG
+    if args.pingpong and NWAVES == 8:
+        PINGPONG = STAGGER = True
         set_geometry(6, 3)
     set_persist(bool(args.persist))
     set_prescale(prescale)

@@ -99,6 +99,7 @@ int64_t fa_query(int what, int64_t a, int64_t b, int64_t c) {
         case FA_QUERY_MASK_ARGS_SIZE: return (int64_t)sizeof(FaBlockMask);
         case FA_QUERY_PAD_WORKSPACE: return a * (int64_t)sizeof(int32_t);
         case FA_QUERY_ROTARY_ARGS_SIZE: return (int64_t)sizeof(FaRotaryArgs);
+        case FA_QUERY_ASM_LAUNCHES: return fa::asm_launch_count();
         case FA_QUERY_BWD_WORKSPACE_NEEDED: {
             // a = head_dim, b = p_dropout > 0, c = block-sparse: 1 if fa_bwd needs dq_accum
             FaBwdArgs t{};

@@ -102,6 +102,8 @@ struct DevFns {
 };
 std::mutex g_mu;
 DevFns g_fns[kMaxDev];
+// assembly-forward launches enqueued (or captured) by this process: fa_query(FA_QUERY_ASM_LAUNCHES)
+std::atomic<int64_t> g_asm_launches{0};
 
 // Every form of the device is loaded at its first asm call, under the mutex, so that after any one
 // eager call no later call (whatever form its grid picks) loads a module: a call inside a hipGraph
@@ -322,7 +324,11 @@ hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavaila
         e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, w8 ? 2 * kRows : kRows, 1, 1, 0,
                                   stream, nullptr, config);
     if (e != hipSuccess) return e;
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e == hipSuccess) g_asm_launches.fetch_add(1, std::memory_order_relaxed);
+    return e;
 }
+
+int64_t asm_launch_count() { return g_asm_launches.load(std::memory_order_relaxed); }
 
 }  // namespace fa

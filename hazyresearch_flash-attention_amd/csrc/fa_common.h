@@ -28,6 +28,23 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// The backward's masking relies on IEEE infinities: rows past seqlen_q and dead block-sparse rows
+// carry lse = +inf so that exp2 gives P = 0, and mask_min() is fminf(p, inf) on live elements. A
+// finite-math build (-ffast-math, -ffinite-math-only) may fold both and unmask those rows.
+#if defined(__FINITE_MATH_ONLY__) && __FINITE_MATH_ONLY__
+#error "fa kernels need IEEE inf semantics (lse = +inf row masking, mask_min): build without -ffinite-math-only"
+#endif
+
+// Timing probes of the backward kernels (FA_BWD_PROBE, FA_BWD_PROBE_NOATOMIC, FA_BWD_SPLIT_PROBE)
+// compute wrong gradients by design. They compile only in an explicit A/B probe build
+// (-DFA_AB_PROBE_BUILD, tools only; build.py refuses to write the product library with one set).
+#if !defined(FA_AB_PROBE_BUILD)
+#if (defined(FA_BWD_PROBE) && FA_BWD_PROBE != 0) || defined(FA_BWD_PROBE_NOATOMIC) || \
+    (defined(FA_BWD_SPLIT_PROBE) && FA_BWD_SPLIT_PROBE != 0)
+#error "backward timing probe set without -DFA_AB_PROBE_BUILD: such a library computes wrong gradients"
+#endif
+#endif
+
 // 16-bit element traits: storage is raw 16-bit, MFMA operand type differs by dtype.
 struct Bf16 {
     typedef bf16x8 frag;
@@ -89,6 +106,7 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 // p (an exp2 result, >= 0) forced to 0 where `masked`: min(p, masked ? 0 : inf). Written as a
 // select of `p` itself, the compiler sank the exp into the unmasked arm and gave every element
 // its own divergent branch; the min keeps the exp on both arms, so the mask stays two VALU ops.
+// (IEEE inf required: see the finite-math guard at the top of this file)
 __device__ __forceinline__ float mask_min(float p, bool masked) { return fminf(p, masked ? 0.f : INFINITY); }
 
 // XCD-aware work order. The dispatcher hands workgroup L (linear id) to XCD L & 7, and each XCD

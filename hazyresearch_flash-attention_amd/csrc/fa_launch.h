@@ -43,6 +43,8 @@ const char *asm_kernel_name(const FaFwdArgs &a);
 // *unavailable is set (and hipSuccess returned, nothing launched) when the device's code objects
 // could not be loaded: the caller then runs the HIP kernels (fa_asm.cpp load_all).
 hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavailable);
+// assembly-forward launches this process has enqueued or captured so far (fa_query)
+int64_t asm_launch_count();
 
 // Raise a kernel's dynamic-LDS limit once per (kernel, device): the attribute is per device, so
 // a process that launches on several GPUs sets it on each. `done` is the call site's own bit set

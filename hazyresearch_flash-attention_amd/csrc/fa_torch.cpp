@@ -418,7 +418,7 @@ void rotary_call(const at::Tensor &x, const at::Tensor &y, const at::Tensor &cos
 // True when fa_fwd takes an assembly kernel for the unrotated dense call of this shape
 // (include/fa_hip.h fa_fwd_kernel_name).
 bool asm_forward_for(int64_t B, int64_t S, int64_t H, int64_t D, double p, bool causal, double scale,
-                     at::ScalarType t) {
+                     at::ScalarType t, int64_t impl) {
     FaFwdArgs a{};
     a.q_row_stride = a.k_row_stride = a.v_row_stride = 3 * H * D;
     a.o_row_stride = H * D;
@@ -432,24 +432,30 @@ bool asm_forward_for(int64_t B, int64_t S, int64_t H, int64_t D, double p, bool 
     a.p_dropout = (float)p;
     a.is_causal = causal ? 1 : 0;
     a.dtype = dtype_code(t);
-    a.impl = FA_IMPL_AUTO;
+    a.impl = (int32_t)impl;
     const char *name = fa_fwd_kernel_name(&a);
     return name != nullptr && std::strstr(name, "_asm") != nullptr;
 }
 
 // FlashAttnRotaryQKVFunc (flash_attention.py): padded contiguous qkv (B, S, 3, H, D); k rotated by
 // one fa_rotary pass, q rotated inside the forward at its load; backward rotates q once more, runs
-// the attention backward on (q_rot, k_rot, v) and rotates dq, dk back in place.
+// the attention backward on (q_rot, k_rot, v) and rotates dq, dk back in place. `impl` is the
+// caller's effective kernel family (flash_attn_hip.force_impl): the route (assembly forward on a
+// pre-rotated q/k buffer, or the HIP forward rotating q at its load) is decided for the kernel
+// that call will really take, and the forward is launched with the same impl.
+// Activation memory: on the assembly route the saved tensor is the (B, S, 2, H, D) rotated q/k
+// buffer (one B*S*H*D 16-bit tensor more than the HIP route's rotated k), which saves the
+// backward's q rotary pass.
 struct FlashAttnRotaryQKVFn : public torch::autograd::Function<FlashAttnRotaryQKVFn> {
     static variable_list forward(AutogradContext *ctx, const at::Tensor &qkv, const at::Tensor &cos_in,
                                  const at::Tensor &sin_in, const at::Tensor &cu, double p, double scale, bool causal,
-                                 uint64_t seed, uint64_t offset, const c10::optional<at::Tensor> &od) {
+                                 uint64_t seed, uint64_t offset, const c10::optional<at::Tensor> &od, int64_t impl) {
         TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.is_contiguous(), "qkv must be contiguous (B, S, 3, H, D)");
         const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
         c10::DeviceGuard guard(qkv.device());
         at::Tensor cos = cos_in.slice(0, 0, S).contiguous(), sin = sin_in.slice(0, 0, S).contiguous();
         at::Tensor flat = qkv.view({B * S, 3, H, D});
-        if (asm_forward_for(B, S, H, D, p, causal, scale, qkv.scalar_type())) {
+        if (asm_forward_for(B, S, H, D, p, causal, scale, qkv.scalar_type(), impl)) {
             // the Q rotation at the kernel's Q load exists in the HIP forward only: where fa_fwd takes an
             // assembly kernel, one fa_rotary pass rotates q and k into (B, S, 2, H, D) and the assembly
             // forward reads them (the backward reuses both rotated tensors: no second q pass)
@@ -458,7 +464,7 @@ struct FlashAttnRotaryQKVFn : public torch::autograd::Function<FlashAttnRotaryQK
                         {S * 2 * H * D, 2 * H * D, H * D, D}, 2, false);
             at::Tensor qk = qk_rot.view({B * S, 2, H, D});
             auto r = fwd(qk.select(1, 0), qk.select(1, 1), flat.select(1, 2), cu, cu, S, S, p, scale, false, causal,
-                         false, seed, offset, od_ptr(od), FA_IMPL_AUTO);
+                         false, seed, offset, od_ptr(od), impl);
             ctx->save_for_backward({qkv, qk_rot, r[0], r[1], cos, sin, cu});
             save_cfg(ctx, S, S, p, scale, causal, seed, offset, od);
             return {r[0].view({B, S, H, D})};
@@ -467,7 +473,7 @@ struct FlashAttnRotaryQKVFn : public torch::autograd::Function<FlashAttnRotaryQK
         rotary_call(qkv.select(2, 1), k_rot, cos, sin, {B, S, 1, H, D}, {S * 3 * H * D, 3 * H * D, 0, D},
                     {S * H * D, H * D, 0, D}, 1, false);
         auto r = fwd(flat.select(1, 0), k_rot.view({B * S, H, D}), flat.select(1, 2), cu, cu, S, S, p, scale, false,
-                     causal, false, seed, offset, od_ptr(od), FA_IMPL_AUTO, cos, sin);
+                     causal, false, seed, offset, od_ptr(od), impl, cos, sin);
         ctx->save_for_backward({qkv, k_rot, r[0], r[1], cos, sin, cu});
         save_cfg(ctx, S, S, p, scale, causal, seed, offset, od);
         return {r[0].view({B, S, H, D})};
@@ -498,7 +504,7 @@ struct FlashAttnRotaryQKVFn : public torch::autograd::Function<FlashAttnRotaryQK
         const std::array<int64_t, 4> st3{S * 3 * H * D, 3 * H * D, H * D, D};
         rotary_call(dqkv, dqkv, cos, sin, {B, S, 3, H, D}, st3, st3, 2, true);   // dq, dk back; dv as is
         at::Tensor n;
-        return {dqkv, n, n, n, n, n, n, n, n, n};
+        return {dqkv, n, n, n, n, n, n, n, n, n, n};
     }
 };
 
@@ -546,8 +552,9 @@ PYBIND11_MODULE(_fa_C, m) {
           });
     m.def("flash_attn_rotary_qkv_func",
           [](const at::Tensor &qkv, const at::Tensor &cos, const at::Tensor &sin, const at::Tensor &cu, double p,
-             double scale, bool causal, uint64_t seed, uint64_t offset, const c10::optional<at::Tensor> &od) {
-              return FlashAttnRotaryQKVFn::apply(qkv, cos, sin, cu, p, scale, causal, seed, offset, od)[0];
+             double scale, bool causal, uint64_t seed, uint64_t offset, const c10::optional<at::Tensor> &od,
+             int64_t impl) {
+              return FlashAttnRotaryQKVFn::apply(qkv, cos, sin, cu, p, scale, causal, seed, offset, od, impl)[0];
           });
     m.def("version", [] { return std::string(fa_version()); });
 }

@@ -69,7 +69,7 @@ class FlashAttnRotaryQKVFunc:
         seed, offset, od = hip._rng_args(dropout_p, qkv.device)
         return C.flash_attn_rotary_qkv_func(qkv, cos, sin, _uniform_cu_seqlens(B, S, qkv.device), dropout_p,
                                             D ** -0.5 if softmax_scale is None else softmax_scale, causal,
-                                            seed, offset, od)
+                                            seed, offset, od, hip._impl())
 
 
 class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
@@ -96,7 +96,10 @@ class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
         rng_state = _reserve(dropout_p, qkv.device)
         flat = qkv.view(B * S, 3, H, D)
         cu = _uniform_cu_seqlens(B, S, qkv.device)
-        name = hip.fwd_kernel_name(B, H, D, S, S, qkv.dtype, causal, dropout_p, row_elems=3 * H * D)
+        # the route follows the kernel this call will really take: the thread's force_impl applies
+        # to the route decision and to the forward alike
+        impl = hip._impl()
+        name = hip.fwd_kernel_name(B, H, D, S, S, qkv.dtype, causal, dropout_p, row_elems=3 * H * D, impl=impl)
         if name is not None and name.endswith("_asm"):
             # the Q rotation at the Q load exists in the HIP forward only: where fa_fwd takes an
             # assembly kernel, one fa_rotary pass rotates q and k (B, S, 2, H, D) and the assembly
@@ -106,14 +109,15 @@ class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
                        (S * 2 * H * D, 2 * H * D, H * D, D), 2, False)
             qk = qk_rot.view(B * S, 2, H, D)
             out, lse = hip.fwd(qk[:, 0], qk[:, 1], flat[:, 2], cu, cu, S, S, dropout_p, softmax_scale,
-                               False, causal, False, None, rng_state=rng_state)
+                               False, causal, False, None, rng_state=rng_state, impl=impl)
             k_rot = qk_rot
         else:
             st = (S * 3 * H * D, 3 * H * D, 0, D)
             k_rot = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
             hip.rotary(qkv[:, :, 1], k_rot, cos, sin, (B, S, 1, H, D), st, (S * H * D, H * D, 0, D), 1, False)
             out, lse = hip.fwd(flat[:, 0], k_rot.view(B * S, H, D), flat[:, 2], cu, cu, S, S, dropout_p,
-                               softmax_scale, False, causal, False, None, rng_state=rng_state, rotary=(cos, sin))
+                               softmax_scale, False, causal, False, None, rng_state=rng_state, rotary=(cos, sin),
+                               impl=impl)
         ctx.save_for_backward(qkv, k_rot, out, lse, cos, sin, cu)
         ctx.rng_state, ctx.dropout_p, ctx.softmax_scale, ctx.causal = rng_state, dropout_p, softmax_scale, causal
         return out.view(B, S, H, D)

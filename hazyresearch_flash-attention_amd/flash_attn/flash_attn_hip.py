@@ -43,6 +43,7 @@ FA_QUERY_MASK_ARGS_SIZE = 6
 FA_QUERY_PAD_WORKSPACE = 7
 FA_QUERY_ROTARY_ARGS_SIZE = 8
 FA_QUERY_BWD_WORKSPACE_NEEDED = 9
+FA_QUERY_ASM_LAUNCHES = 10
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -612,6 +613,12 @@ def rotary(x, y, cos, sin, shape, x_strides, y_strides, nrot, inverse):
     if rc != 0:
         _raise(rc, "fa_rotary")
     return y
+
+
+def asm_launch_count():
+    """Assembly-forward launches this process has enqueued or captured (fa_query FA_QUERY_ASM_LAUNCHES):
+    diagnostics of which kernel family a call or a graph capture took."""
+    return int(lib().fa_query(FA_QUERY_ASM_LAUNCHES, 0, 0, 0))
 
 
 def fwd_kernel_name(batch, nheads, head_dim, max_seqlen_q, max_seqlen_k, dtype=torch.bfloat16, causal=False,

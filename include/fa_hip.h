@@ -233,6 +233,8 @@ enum {
     FA_QUERY_ROTARY_ARGS_SIZE = 8,   /* sizeof(FaRotaryArgs) */
     FA_QUERY_BWD_WORKSPACE_NEEDED = 9,   /* a = head_dim, b = (p_dropout > 0), c = block-sparse
                                             -> 1 if fa_bwd reads dq_accum, 0 if dq is written directly */
+    FA_QUERY_ASM_LAUNCHES = 10,   /* -> assembly-forward launches this process has enqueued or captured
+                                     (diagnostics: which kernel family a call, or a graph capture, took) */
 };
 int64_t fa_query(int what, int64_t a, int64_t b, int64_t c);
 

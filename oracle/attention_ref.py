@@ -12,6 +12,11 @@ Follows /root/reference/tests/test_flash_attn.py:
                                           give 0 instead of NaN, as the kernels do)
 The reference's attention_ref raises UnboundLocalError when dropout_mask is None (:153-155);
 here a missing mask means "keep everything".
+
+And /root/reference/benchmarks/benchmark_flash_attention.py:
+  attention_pytorch_bench       :14-36   (the benchmark's naive PyTorch attention on packed qkv: the
+                                          CPU baseline bench.py times, torch.utils.benchmark.Timer as
+                                          benchmarks/utils.py:8-20 does)
 """
 import math
 
@@ -141,3 +146,23 @@ def attention_blocksparse_ref(qkv, blockmask, attn_mask=None, dropout_p=0.0, dro
     if attn_mask is not None:
         output.masked_fill_(~attn_mask[:, :, None, None], 0.0)
     return output.to(dtype=dtype_og), attention.to(dtype=dtype_og)
+
+
+def attention_pytorch_bench(qkv, attn_mask=None, dropout_p=0.0, upcast=False, causal=False):
+    """The reference benchmark's naive attention (benchmarks/benchmark_flash_attention.py:14-36):
+    qkv (B, S, 3, H, D), attn_mask (B, S) bool (True = valid, None = all valid). Scores are
+    q . (k / sqrt(d)), masked keys and (causal) the upper triangle get -inf, softmax, dropout by
+    F.dropout, then P V; the output comes back in qkv's dtype."""
+    import torch.nn.functional as F
+    q, k, v = (qkv.float() if upcast else qkv).unbind(dim=2)
+    seqlen, d = qkv.shape[1], qkv.shape[-1]
+    scores = torch.einsum("bthd,bshd->bhts", q, k / math.sqrt(d))
+    if attn_mask is not None:
+        scores.masked_fill_(~attn_mask[:, None, None, :], float("-inf"))
+    if causal:
+        cm = torch.triu(torch.ones(seqlen, seqlen, dtype=torch.bool, device=qkv.device), 1)
+        scores.masked_fill_(cm, float("-inf"))
+    attention = torch.softmax(scores, dim=-1)
+    attention_drop = F.dropout(attention, dropout_p)
+    output = torch.einsum("bhts,bshd->bthd", attention_drop, v)
+    return output.to(dtype=qkv.dtype)

@@ -169,3 +169,19 @@ def test_max_err_bound_floor():
     a = torch.zeros(3)
     assert max_err_bound(a, a) == 0.0
     assert max_err_bound(a, a, floor=1e-5) == 1e-5
+
+
+def test_benchmark_attention_restatement_matches_attention_ref():
+    """oracle.attention_pytorch_bench (the reference benchmark's naive attention, bench.py's CPU
+    baseline: benchmarks/benchmark_flash_attention.py:14-36) computes what the pinned attention_ref
+    computes with the scale on k (reorder_ops), bit for bit at fp32, with a key mask and causal."""
+    from oracle.attention_ref import attention_pytorch_bench, attention_ref
+    g = torch.Generator().manual_seed(3)
+    B, S, H, D = 2, 96, 3, 32
+    qkv = torch.randn(B, S, 3, H, D, generator=g)
+    mask = torch.arange(S)[None, :] < torch.tensor([[S], [S - 17]])
+    for causal in (False, True):
+        out = attention_pytorch_bench(qkv, mask, 0.0, upcast=True, causal=causal)
+        q, k, v = qkv.unbind(2)
+        ref, _ = attention_ref(q, k, v, key_padding_mask=mask, causal=causal, reorder_ops=True)
+        assert torch.equal(out, ref)
