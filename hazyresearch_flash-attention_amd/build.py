@@ -37,7 +37,6 @@ ASM_GEN = os.path.join(CSRC, "asm", "gen_fwd.py")
 # (dtype, head-dim tile, waves per workgroup or "p" = the persistent 4-wave form, symbol)
 ASM_KERNELS = [("bf16", 64, 4, "fa_asm_fwd_d64_bf16"), ("f16", 64, 4, "fa_asm_fwd_d64_f16"),
                ("bf16", 128, 4, "fa_asm_fwd_d128_bf16"), ("f16", 128, 4, "fa_asm_fwd_d128_f16"),
-               ("bf16", 64, 8, "fa_asm_fwd_d64w8_bf16"), ("f16", 64, 8, "fa_asm_fwd_d64w8_f16"),
                ("bf16", 64, "p", "fa_asm_fwd_d64p_bf16"), ("f16", 64, "p", "fa_asm_fwd_d64p_f16"),
                ("bf16", 128, "p", "fa_asm_fwd_d128p_bf16"), ("f16", 128, "p", "fa_asm_fwd_d128p_f16"),
                ("bf16", 96, 4, "fa_asm_fwd_d96_bf16"), ("f16", 96, 4, "fa_asm_fwd_d96_f16"),

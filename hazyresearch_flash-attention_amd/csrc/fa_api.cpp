@@ -80,6 +80,7 @@ const char *fa_fwd_kernel_name(const FaFwdArgs *a) {
     if (a == nullptr || a->head_dim <= 0 || a->head_dim > 128 || a->head_dim % 8 != 0 || a->batch <= 0 ||
         a->nheads <= 0 || a->max_seqlen_q <= 0 || a->max_seqlen_k < 0 ||
         (a->dtype != FA_DTYPE_FP16 && a->dtype != FA_DTYPE_BF16) || a->impl < FA_IMPL_AUTO || a->impl > FA_IMPL_ASM4P ||
+        a->impl == FA_IMPL_ASM8 ||
         a->p_dropout < 0.f || a->p_dropout >= 1.f)
         return nullptr;
     if (fa::fwd_asm_eligible(*a, FaBlockMask{nullptr, 0, 0, 0})) return fa::asm_kernel_name(*a);
@@ -159,8 +160,9 @@ int fwd_impl(const FaFwdArgs *a, const FaBlockMask &bm, void *stream) {
     if ((int64_t)a->max_seqlen_q * a->q_row_stride * 2 >= lim || (int64_t)a->max_seqlen_k * a->k_row_stride * 2 >= lim ||
         (int64_t)a->max_seqlen_k * a->v_row_stride * 2 >= lim)
         return fail(FA_ERR_UNSUPPORTED, "fa_fwd: a sequence spans more than 2 GiB (seqlen * row_stride)");
-    if (a->impl < FA_IMPL_AUTO || a->impl > FA_IMPL_ASM4P)
-        return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: impl must be one of FA_IMPL_AUTO / HIP / ASM4 / ASM8 / ASM4P");
+    if (a->impl < FA_IMPL_AUTO || a->impl > FA_IMPL_ASM4P || a->impl == FA_IMPL_ASM8)
+        return fail(FA_ERR_INVALID_ARGUMENT, "fa_fwd: impl must be one of FA_IMPL_AUTO / HIP / ASM4 / ASM4P "
+                                             "(FA_IMPL_ASM8 is not in this library)");
     if (a->max_seqlen_q == 0) return FA_OK;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipSuccess;

@@ -27,10 +27,6 @@ extern const unsigned char fa_asm_fwd_d128_bf16[];
 extern const unsigned long fa_asm_fwd_d128_bf16_size;
 extern const unsigned char fa_asm_fwd_d128_f16[];
 extern const unsigned long fa_asm_fwd_d128_f16_size;
-extern const unsigned char fa_asm_fwd_d64w8_bf16[];
-extern const unsigned long fa_asm_fwd_d64w8_bf16_size;
-extern const unsigned char fa_asm_fwd_d64w8_f16[];
-extern const unsigned long fa_asm_fwd_d64w8_f16_size;
 extern const unsigned char fa_asm_fwd_d64p_bf16[];
 extern const unsigned long fa_asm_fwd_d64p_bf16_size;
 extern const unsigned char fa_asm_fwd_d64p_f16[];
@@ -93,9 +89,11 @@ constexpr int kRows = 256;            // query rows per workgroup
 constexpr int kMaxDev = 64;
 constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
 
-// kernels: [form (0: D=64, 1: D=128, 2: D=64 two waves per SIMD, 3: D=64 persistent, 4: D=128
-// persistent, 5: D=96, 6: D=96 persistent) * 2 + dtype (0: bf16, 1: f16)]
-constexpr int kNumFns = 14;
+// kernels: [form (0: D=64, 1: D=128, 2: D=64 persistent, 3: D=128 persistent, 4: D=96, 5: D=96
+// persistent) * 2 + dtype (0: bf16, 1: f16)]. The two-waves-per-SIMD form (gen_fwd.py --waves 8,
+// FA_IMPL_ASM8) measured even or slower in every A/B and left the library in
+// round 6; the generator keeps it for A/B builds.
+constexpr int kNumFns = 12;
 struct DevFns {
     hipModule_t mod[kNumFns] = {};
     hipFunction_t fn[kNumFns] = {};
@@ -116,14 +114,12 @@ std::atomic<int64_t> g_asm_launches{0};
 hipError_t load_all(DevFns &d, int want) {
     static const void *const imgs[kNumFns] = {fa_asm_fwd_d64_bf16,   fa_asm_fwd_d64_f16,
                                               fa_asm_fwd_d128_bf16,  fa_asm_fwd_d128_f16,
-                                              fa_asm_fwd_d64w8_bf16, fa_asm_fwd_d64w8_f16,
                                               fa_asm_fwd_d64p_bf16,  fa_asm_fwd_d64p_f16,
                                               fa_asm_fwd_d128p_bf16, fa_asm_fwd_d128p_f16,
                                               fa_asm_fwd_d96_bf16,   fa_asm_fwd_d96_f16,
                                               fa_asm_fwd_d96p_bf16,  fa_asm_fwd_d96p_f16};
     static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
                                                "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
-                                               "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
                                                "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
                                                "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm",
                                                "fa_fwd_d96_bf16_asm",   "fa_fwd_d96_f16_asm",
@@ -201,10 +197,6 @@ bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
     return true;
 }
 
-// The two-waves-per-SIMD form (8-wave workgroups, one 32-row block per wave) serves head_dim == 64
-// only (its Q loads and O stores address whole rows from one base); measured even with the
-// one-wave form, it runs only when forced.
-static bool use_w8(const FaFwdArgs &a) { return a.head_dim == 64 && a.impl == FA_IMPL_ASM8; }
 
 // CUs of the current device rounded down to whole XCD rounds (8): the persistent grid, so that
 // workgroup P walks L = P, P + G, ... in the XCD-aware block order of the one-block launch.
@@ -228,7 +220,7 @@ static int persist_grid() {
 // Every form computes fp32-exact scores (round 5: the pre-scaled Q of round 4, gen_fwd.py PRESCALE,
 // is out of the product), so the choice is by grid shape only, never by key count.
 static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
-    if (a.is_causal || a.impl == FA_IMPL_ASM4 || a.impl == FA_IMPL_ASM8) return 0;
+    if (a.is_causal || a.impl == FA_IMPL_ASM4) return 0;
     const int g = persist_grid();
     if (g < 8) return 0;
     if (a.impl == FA_IMPL_ASM4P) return (int)(nwg < (uint32_t)g ? nwg : (uint32_t)g);
@@ -238,17 +230,15 @@ static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
 // The code object launch_fwd_asm runs for these arguments (form index of kNumFns / 2) and the
 // persistent grid (0: one workgroup per block).
 static int asm_form(const FaFwdArgs &a, int *pgrid) {
-    const bool w8 = use_w8(a);
     const uint32_t nqb0 = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
-    *pgrid = w8 ? 0 : persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
+    *pgrid = persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
     const bool d128 = a.head_dim > 96, d96 = a.head_dim > 64 && !d128;
-    return w8 ? 2 : *pgrid ? (d128 ? 4 : d96 ? 6 : 3) : (d128 ? 1 : d96 ? 5 : 0);
+    return *pgrid ? (d128 ? 3 : d96 ? 5 : 2) : (d128 ? 1 : d96 ? 4 : 0);
 }
 
 const char *asm_kernel_name(const FaFwdArgs &a) {
     static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
                                                "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
-                                               "fa_fwd_d64w8_bf16_asm", "fa_fwd_d64w8_f16_asm",
                                                "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
                                                "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm",
                                                "fa_fwd_d96_bf16_asm",   "fa_fwd_d96_f16_asm",
@@ -260,7 +250,6 @@ const char *asm_kernel_name(const FaFwdArgs &a) {
 hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavailable) {
     hipFunction_t fn = nullptr;
     *unavailable = false;
-    const bool w8 = use_w8(a);
     int pgrid = 0;
     const int form = asm_form(a, &pgrid);
     hipError_t e = get_function(a.dtype, form, &fn);
@@ -321,8 +310,8 @@ hipError_t launch_fwd_asm(const FaFwdArgs &a, hipStream_t stream, bool *unavaila
     if (pgrid)
         e = hipModuleLaunchKernel(fn, (unsigned)pgrid, 1, 1, kRows, 1, 1, 0, stream, nullptr, config);
     else
-        e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, w8 ? 2 * kRows : kRows, 1, 1, 0,
-                                  stream, nullptr, config);
+        e = hipModuleLaunchKernel(fn, nqb, (unsigned)a.nheads, (unsigned)a.batch, kRows, 1, 1, 0, stream, nullptr,
+                                  config);
     if (e != hipSuccess) return e;
     e = hipGetLastError();
     if (e == hipSuccess) g_asm_launches.fetch_add(1, std::memory_order_relaxed);

@@ -75,7 +75,7 @@ class FaFwdArgs(ctypes.Structure):
 FA_IMPL_AUTO = 0
 FA_IMPL_HIP = 1
 FA_IMPL_ASM4 = 2    # the one-wave-per-SIMD assembly forward where eligible (tests, A/B)
-FA_IMPL_ASM8 = 3    # the two-waves-per-SIMD assembly forward where eligible (head_dim == 64)
+FA_IMPL_ASM8 = 3    # reserved: the two-waves-per-SIMD form is an A/B generator build, not in the library
 FA_IMPL_ASM4P = 4   # the persistent one-wave-per-SIMD assembly forward where eligible (non-causal)
 
 

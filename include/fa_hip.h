@@ -109,11 +109,12 @@ typedef struct FaFwdArgs {
     /* Kernel family (FA_IMPL_*). FA_IMPL_AUTO picks the fastest kernel for the shape: the
      * hand-scheduled assembly forward for head_dim in (32, 64], 80, 96 or 128, fp16/bf16, no dropout,
      * dense, no fused rotary (non-causal grids with more blocks than CUs take its persistent form); the
-     * HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels; FA_IMPL_ASM4 / FA_IMPL_ASM8 /
-     * FA_IMPL_ASM4P force the one-wave-per-SIMD, the two-waves-per-SIMD and the persistent
-     * one-wave-per-SIMD assembly form where the shape is eligible. The three assembly forms compute the
-     * same fp32-exact scores and sums in the same order (bitwise equal outputs); the HIP kernels differ
-     * from them in the last bits (summation order), all within the reference's 2x rule. */
+     * HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels; FA_IMPL_ASM4 / FA_IMPL_ASM4P force
+     * the one-wave-per-SIMD assembly form, one workgroup per block or persistent, where the shape is
+     * eligible. The assembly forms compute the same fp32-exact scores and sums in the same order
+     * (bitwise equal outputs); the HIP kernels differ from them in the last bits (summation order),
+     * all within the reference's 2x rule. FA_IMPL_ASM8 (the two-waves-per-SIMD form, an A/B build of
+     * the generator since round 6) is reserved: fa_fwd rejects it with FA_ERR_INVALID_ARGUMENT. */
     int32_t impl;
     int32_t reserved;         /* 0 */
 } FaFwdArgs;

@@ -41,6 +41,7 @@ def test_struct_layouts_match():
     assert L.fa_query(hip.FA_QUERY_MAX_HEAD_DIM, 0, 0, 0) == 128
     assert L.fa_query(hip.FA_QUERY_BWD_WORKSPACE, 10, 2, 64) == 10 * 2 * 64 * 4
     assert L.fa_query(999, 0, 0, 0) == -1
+    assert L.fa_query(hip.FA_QUERY_ASM_LAUNCHES, 0, 0, 0) == hip.asm_launch_count() >= 0
     assert b"gfx950" in L.fa_version()
 
 
@@ -63,6 +64,7 @@ def _valid_fwd_args(hip):
     ("p_dropout", 1.0, 1), ("p_dropout", -0.1, 1), ("lse_stride", -1, 1), ("cu_seqlens_q", None, 1),
     ("q_row_stride", 129, 1), ("softmax_scale", float("inf"), 1),
     ("q_row_stride", 0, 1), ("k_row_stride", 8, 1),      # broadcast / overlapping rows
+    ("impl", 3, 1), ("impl", 5, 1), ("impl", -1, 1),     # FA_IMPL_ASM8 is reserved (not in the library)
 ])
 def test_fwd_argument_validation(field, value, code):
     from flash_attn import flash_attn_hip as hip

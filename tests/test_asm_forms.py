@@ -1,6 +1,6 @@
 """GPU parity of each hand-scheduled assembly forward form, forced through FaFwdArgs.impl
-(include/fa_hip.h): FA_IMPL_ASM4 (one wave per SIMD, two 32-row blocks per wave) and FA_IMPL_ASM8
-(two waves per SIMD, one block per wave, head_dim == 64), against the fp32 oracle under the
+(include/fa_hip.h): FA_IMPL_ASM4 (one wave per SIMD, two 32-row blocks per wave, one workgroup per
+block) and FA_IMPL_ASM4P (the same body in the persistent form), against the fp32 oracle under the
 reference's 2x rule (/root/reference/tests/test_flash_attn.py:407-409) and the LSE tolerance of
 tests/test_flash_attn.py, so both forms stay green whichever one FA_IMPL_AUTO picks."""
 import pytest
@@ -20,7 +20,7 @@ def _hip():
     return hip
 
 
-@pytest.mark.parametrize("form", ["ASM4", "ASM8", "ASM4P"])
+@pytest.mark.parametrize("form", ["ASM4", "ASM4P"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("seqlen_q,seqlen_k", [(97, 97), (257, 513), (512, 512), (1025, 300), (2048, 2048)])
@@ -30,7 +30,7 @@ def test_asm_form_forward(form, dtype, causal, seqlen_q, seqlen_k):
         run_case("separate", 3, seqlen_q, seqlen_k, 4, 64, dtype, causal, 0.0, grad=False, seed=seqlen_q)
 
 
-@pytest.mark.parametrize("form", ["ASM4", "ASM8", "ASM4P"])
+@pytest.mark.parametrize("form", ["ASM4", "ASM4P"])
 def test_asm_form_forced_rescale(form):
     """A spike key that row 7 meets only in a later tile: the out-of-line rescale block."""
     from flash_attn import flash_attn_interface as fi
@@ -51,7 +51,7 @@ def test_asm_form_forced_rescale(form):
 
 def test_asm_forms_agree_at_north_star_grid():
     """B=8 H=12 S=2048 D=64 bf16 (the bench workload, 768 blocks: three per CU in the persistent
-    form): the three forms compute the same fp32-exact scores and sums in the same order, so their
+    form): the two forms compute the same fp32-exact scores and sums in the same order, so their
     outputs are bitwise equal, and every form matches fp32."""
     from flash_attn import flash_attn_interface as fi
     hip = _hip()
@@ -60,10 +60,9 @@ def test_asm_forms_agree_at_north_star_grid():
     q, k, v = (torch.randn(B * S, H, d, generator=g).bfloat16().to(DEV) for _ in range(3))
     cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=DEV)
     outs = {}
-    for form in ("ASM4", "ASM8", "ASM4P"):
+    for form in ("ASM4", "ASM4P"):
         with hip.force_impl(getattr(hip, f"FA_IMPL_{form}")):
             outs[form] = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0, return_attn_probs=False)
-    assert torch.equal(outs["ASM4"], outs["ASM8"])     # same arithmetic in the same order
     assert torch.equal(outs["ASM4"], outs["ASM4P"])
     # against fp32 on two heads of the first sequence
     qf, kf, vf = (x[:S, :2].float().transpose(0, 1) for x in (q, k, v))

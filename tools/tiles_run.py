@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--mode", required=True, choices=["fwd", "bwd"])
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--warm", type=float, default=0.3)
-    ap.add_argument("--impl", default="auto", choices=["auto", "hip", "asm4", "asm8", "asm4p"],
+    ap.add_argument("--impl", default="auto", choices=["auto", "hip", "asm4", "asm4p"],
                     help="forward kernel family (FaFwdArgs.impl)")
     a = ap.parse_args()
     if a.cfg in CFGS:
