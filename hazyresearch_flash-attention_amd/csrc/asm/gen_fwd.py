@@ -80,6 +80,12 @@ ORDET_ANDOR = True     # ORDET: the last P word enters the test by one v_and_or_
 PHASE_TAIL = 1         # ORDET test issued before the phase's last PHASE_TAIL MFMAs, its branch after them
 
 
+def soff_walk():
+    """SOFF_WALK applies to every form but the persistent forms with the next-block K/V tail
+    (PERSIST_KV: D = 96 / 128), whose tail DMAs walk the next block's descriptor sets."""
+    return SOFF_WALK and not (PERSIST and PERSIST_KV)
+
+
 def set_geometry(r, dist):
     """Ring of r slots per tensor, DMA distance dist (<= r - 1: a slot is rewritten only after
     the barrier that follows its last read); the loop unroll is lcm(r, 2)."""
@@ -276,6 +282,12 @@ def epi_regs(X, idx):
 # ---- SGPRs
 S_KD, S_VD, S_QD, S_OD, S_LD = 8, 12, 16, 20, 24   # buffer descriptors (4 each)
 S_KD1, S_VD1 = 80, 84  # second K / V descriptor sets (odd tiles; prologue temporaries before)
+# SOFF_WALK (round 6): one K and one V descriptor per block, the tile selected by the SGPR offset of
+# the DMA (the raw-buffer range check includes it on gfx950: tools/micro/soffset_probe.hip,
+# profiles/r06/soffset_probe.txt), two offsets per tensor (even / odd tiles) each advanced by two
+# tiles right before its next use: one SALU per tensor and tile instead of four, in s80..s83
+S_KOFF, S_VOFF = (80, 81), (82, 83)
+SOFF_WALK = True
 S_C, S_THR, S_J, S_NT, S_LAST = 28, 29, 30, 31, 32
 S_CAUSAL, S_MAGIC_BH = 33, 34   # kernel arguments: causal flag, ceil(2^32 / (2 nbh))
 S_MSTART = 39          # first tile of the masked loop (causal: the diagonal band; else the last tile)
@@ -452,10 +464,25 @@ class Gen:
         still reads (measured -4 % against a walk right behind the DMA)."""
         out = []
         region = KREG if kind == 'K' else VREG
+        step = S_KSTEP if kind == 'K' else S_VSTEP          # 2 tiles of bytes
+        if soff_walk() and not nxt:
+            desc = S_KD if kind == 'K' else S_VD
+            off = (S_KOFF if kind == 'K' else S_VOFF)[t % 2]
+            dregs = [f's{desc + i}' for i in range(4)] + [f's{off}']
+            if t >= 2 and 'nowalk' not in PROBE:
+                out.append(salu(f's_add_u32 s{off}, s{off}, s{step}', rd=[f's{off}', f's{step}'], wr=[f's{off}', 'scc']))
+            if walk_only:
+                return out
+            for i in range(NP):
+                m0 = region + (t % R) * TILE + 1024 * NWAVES * i   # + 1024 * wave (S_M0B)
+                voff = V_DMA + (0 if kind == 'K' else NP) + i
+                out.append(Inst(f's_add_u32 m0, s{S_M0B}, {m0}', 'm0', 2, rd=[f's{S_M0B}'], wr=['m0', 'scc']))
+                out.append(Inst(f'buffer_load_dwordx4 v{voff}, s[{desc}:{desc + 3}], s{off} offen lds', 'dma', 16,
+                                rd=[f'v{voff}', 'm0'] + dregs))
+            return out
         desc = (S_KD if t % 2 == 0 else S_KD1) if kind == 'K' else (S_VD if t % 2 == 0 else S_VD1)
         if nxt:     # the next block's sets (persistent form's tail: t = the next block's tile)
             desc = S_NXD[kind][t % 2]
-        step = S_KSTEP if kind == 'K' else S_VSTEP          # 2 tiles of bytes
         dregs = [f's{desc + i}' for i in range(4)]
         if t >= 2 and 'nowalk' not in PROBE:
             st = f's{step}'
@@ -1376,7 +1403,10 @@ def prologue_sections(g):
           S('s_mul_i32 s84, s81, s82'), S('s_min_u32 s85, s81, s83'), S('s_add_u32 s84, s84, s85'),
           S('s_lshr_b32 s85, s80, 3'), S('s_add_u32 s84, s84, s85'),
           S('s_lshl_b32 s85, s84, 1'), S('s_mul_hi_u32 s86, s85, s72'),
-          S('s_mul_i32 s87, s86, s70'), S('s_sub_u32 s87, s84, s87'),
+          S('s_mul_i32 s87, s86, s70'), S('s_sub_u32 s87, s84, s87')]
+    # (the persistent form runs non-causal grids only: the causal block orders below are not in it;
+    # there s98..s101 hold its own state)
+    p += [] if PERSIST else [
           # causal: global heaviest-first order, rank = L / nbh (s75 = nbh), bh = L - rank nbh,
           # qb = nqb - 1 - rank (the last q-blocks see the most keys)
           S('s_lshl_b32 s85, s80, 1'), S(f's_mul_hi_u32 s81, s85, s{S_MAGIC_BH}'),
@@ -1394,8 +1424,8 @@ def prologue_sections(g):
           S('s_add_u32 s94, s94, s95'),
           S('s_sub_u32 s95, s70, 1'), S('s_sub_u32 s95, s95, s93'),
           S('s_cmp_lg_u32 s98, 0'), S('s_cselect_b32 s82, s94, s82'), S('s_cselect_b32 s83, s95, s83'),
-          S(f's_cmp_lg_u32 s{S_CAUSAL}, 0'), S('s_cselect_b32 s86, s82, s86'), S('s_cselect_b32 s87, s83, s87'),
-          S('s_lshl_b32 s85, s86, 1'), S('s_mul_hi_u32 s88, s85, s73'),
+          S(f's_cmp_lg_u32 s{S_CAUSAL}, 0'), S('s_cselect_b32 s86, s82, s86'), S('s_cselect_b32 s87, s83, s87')]
+    p += [S('s_lshl_b32 s85, s86, 1'), S('s_mul_hi_u32 s88, s85, s73'),
           S('s_mul_i32 s89, s88, s66'), S('s_sub_u32 s89, s86, s89'),
           S('s_lshl_b32 s90, s88, 2'),
           S('s_add_u32 s92, s50, s90'), S('s_addc_u32 s93, s51, 0'),
@@ -1429,8 +1459,16 @@ def prologue_sections(g):
           S(f's_cmp_lg_u32 s{S_CAUSAL}, 0'), S(f's_cselect_b32 s{S_MSTART}, s97, s{S_LAST}'),
           S(f's_lshl_b32 s{S_KSTEP}, s63, 7'), S(f's_lshl_b32 s{S_VSTEP}, s64, 7'),
           S(f's_lshl_b32 s{S_M0B}, s{S_WAVE}, 10')]
-    # second descriptor sets (odd tiles): one tile (64 rows) further, num_records saturating
-    for d0, d1, rs in ((S_KD, S_KD1, 63), (S_VD, S_VD1, 64)):
+    # SOFF_WALK: the DMA offsets of tiles 0 and 1; else second descriptor sets (odd tiles): one tile
+    # (64 rows) further, num_records saturating
+    # (own section: the persistent form with CARRY_DECODE places it after the next block's decode,
+    # whose temporaries include s80..s83)
+    p.append(sec('soffinit'))
+    if soff_walk():
+        p += [S(f's_mov_b32 s{S_KOFF[0]}, 0'), S(f's_lshl_b32 s{S_KOFF[1]}, s63, 6'),
+              S(f's_mov_b32 s{S_VOFF[0]}, 0'), S(f's_lshl_b32 s{S_VOFF[1]}, s64, 6')]
+    p.append(sec('state2'))
+    for d0, d1, rs in ((S_KD, S_KD1, 63), (S_VD, S_VD1, 64)) if not soff_walk() else ():
         p += [S(f's_lshl_b32 s96, s{rs}, 6'),
               S(f's_add_u32 s{d1}, s{d0}, s96'), S(f's_addc_u32 s{d1 + 1}, s{d0 + 1}, 0'),
               S(f's_sub_u32 s{d1 + 2}, s{d0 + 2}, s96'), S(f's_cselect_b32 s{d1 + 2}, 0, s{d1 + 2}'),
@@ -1776,9 +1814,23 @@ def prologue_persist(g):
     dec2 = [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
     if 'dec3' in PROBE:     # timing probe: the current block's decode twice (the price of one decode)
         dec2 = dec2 + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
-    pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + nxt + dec2 + \
-        sc['state'] + lanes_t + \
-        sc['rows'] + pstamp(PS_V + 4, 'pstA') + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
+    if carry_decode():
+        # the block's sequence bounds and (b, h, q-block) come from the previous decode of this block
+        # (the previous block's `nxt`, or for a workgroup's first block pro_a, or the .Lend path): no
+        # second decode with its cu_seqlens loads per block; `nxt` runs after the row offsets
+        restore = [S('s_mov_b32 s76, s84'), S('s_add_u32 s77, s84, s85'), S('s_mov_b32 s78, s0'),
+                   S('s_add_u32 s79, s0, s1'), S(f's_mov_b32 s87, s{S_NQB}'), S('s_mov_b32 s88, s86'),
+                   S('s_mov_b32 s89, s2')]
+        if 'dec3' in PROBE:     # timing probe: one more decode of this block (the price of a decode)
+            restore = [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + restore
+        pro_a += [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + carry_save()
+        pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + restore + sc['state'] + sc['state2'] + lanes_t + sc['rows'] + \
+            nxt + carry_save(after_nxt=True) + sc['soffinit'] + pstamp(PS_V + 4, 'pstA') + \
+            ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
+    else:
+        pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + nxt + dec2 + \
+            sc['state'] + sc['soffinit'] + sc['state2'] + lanes_t + \
+            sc['rows'] + pstamp(PS_V + 4, 'pstA') + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
     qcopy = [Inst(f'v_accvgpr_write_b32 a{A_Q[X] + r}, v{V_QN + 16 * xi + r}', 'accw',
                   rd=[f'v{V_QN + 16 * xi + r}'], wr=[f'a{A_Q[X] + r}'])
              for xi, X in enumerate(BLOCKS) for r in range(16)] + [raw('s_branch .Lqdone')]
@@ -1861,6 +1913,24 @@ def prologue_persist(g):
 
 
 N_STORES = 10         # LSE + O stores per wave of the epilogue (D = 64: 2 x (1 + 4); set_persist)
+CARRY_DECODE = True   # persistent form: a block's decode carried from the previous block's next-block decode
+
+
+def carry_decode():
+    """CARRY_DECODE applies to the persistent forms without the next-block K/V tail (D = 64): the
+    tail's descriptor code (tail_desc) uses s3 as a temporary."""
+    return CARRY_DECODE and PERSIST and not PERSIST_KV and soff_walk()
+
+
+def carry_save(after_nxt=False):
+    """Carry registers of the next block's decode: s0 k start, s1 seqlen_k, s2 head, s3 (S_NQB) q-block,
+    s84 q start, s85 seqlen_q, s86 batch (free from the block's decode to the next block's restore:
+    the loop keeps only its DMA offsets in s80..s83). `nxt` already leaves s0..s3 and s77 = seqlen_q."""
+    out = [S('s_mov_b32 s84, s76'), S('s_mov_b32 s86, s88')]
+    if after_nxt:
+        return out + [S('s_mov_b32 s85, s77')]
+    return out + [S('s_sub_u32 s85, s77, s76'), S(f's_mov_b32 s{S_NQB}, s87'), S('s_mov_b32 s0, s78'),
+                  S('s_sub_u32 s1, s79, s78'), S('s_mov_b32 s2, s89')]
 PERSIST_Q = True      # persistent form: next-block Q prefetch (D = 64 only)
 QCOPY_LATE = True     # persistent PRESCALE: the next-Q copy + scale after the block's first DMAs
 BAR2 = False          # main loop: one barrier per two tiles (needs R >= 6, DIST >= 3, even unroll)
@@ -2191,7 +2261,12 @@ def build(g):
     end = [label('.Lend'), raw('s_endpgm')]
     if PERSIST:
         # .Lend (q-block past its sequence: nothing prefetched) and .Lseam (after a block): next block
-        end = [label('.Lend'), S(f's_mov_b32 s{S_QPF}, 0'), label('.Lseam')] + pstamp_store() + [
+        lend_dec = []
+        if carry_decode():
+            # a q-block past its sequence skipped `nxt`: decode the next block here
+            lend_dec = [S('s_add_u32 s80, s99, s100'), S('s_sub_u32 s81, s71, 1'), S('s_min_u32 s80, s80, s81')] + \
+                [x for x in split_sections(prologue_sections(g))['decode_map']] + carry_save()
+        end = [label('.Lend'), S(f's_mov_b32 s{S_QPF}, 0')] + lend_dec + [label('.Lseam')] + pstamp_store() + [
                S(f's_add_u32 s{S_L}, s{S_L}, s{S_G}'), S(f's_cmp_ge_u32 s{S_L}, s71'), raw('s_cbranch_scc1 .Ldone'),
                raw('s_barrier'), raw('s_branch .Lblock')]
         done = [label('.Ldone'), raw('s_waitcnt vmcnt(0)'), raw('s_endpgm')]
@@ -2397,10 +2472,17 @@ def main():
     ap.add_argument('--andor', type=int, default=None, help='ORDET: last P word joins the test by v_and_or_b32')
     ap.add_argument('--ptail', type=int, default=None, help='rescale test before the last N MFMAs of its phase')
     ap.add_argument('--shift', type=int, default=None, help='loop code placement: N 4-byte s_nop 0 after its alignment')
+    ap.add_argument('--soff', type=int, default=None, help='DMA tiles by the SGPR offset of one descriptor (SOFF_WALK)')
+    ap.add_argument('--carry', type=int, default=None, help="persistent: a block's decode carried from the previous block")
     args = ap.parse_args()
-    global LOOP_SHIFT
+    global LOOP_SHIFT, SOFF_WALK
     if args.shift is not None:
         LOOP_SHIFT = args.shift
+    if args.soff is not None:
+        SOFF_WALK = bool(args.soff)
+    global CARRY_DECODE
+    if args.carry is not None:
+        CARRY_DECODE = bool(args.carry)
     global DUMP
     if args.dump:
         pt, regs = args.dump.split(':')

@@ -43,10 +43,24 @@ def _batch(lens_q, lens_k, H, d, dtype, seed):
 @pytest.mark.parametrize("impl", ["AUTO", "ASM4P"])
 def test_asm_forward_ragged_short_and_long_keys(impl, layout, dtype, scale_mul):
     """scale_mul multiplies the default d^-0.5 = 1/8: 8 gives softmax_scale 1.0, 1/8 gives 1/d."""
+    _ragged_case(impl, layout, dtype, scale_mul, 64)
+
+
+@pytest.mark.parametrize("d", [32, 96, 128])
+@pytest.mark.parametrize("scale_mul", [4.0, 0.25])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_non_default_scale_other_head_dims(d, scale_mul, dtype):
+    """a non-default softmax_scale at the other head-dim tiles (D = 32: the HIP
+    forward; D = 96 / 128: the assembly D = 96 / 128 tiles), the same ragged batch, forward and
+    backward. scale_mul is a power of two, so the oracle sees q rescaled exactly."""
+    _ragged_case("AUTO", "separate", dtype, scale_mul, d)
+
+
+def _ragged_case(impl, layout, dtype, scale_mul, d):
     import contextlib
     from flash_attn import flash_attn_hip as hip
     from flash_attn import flash_attn_interface as fi
-    H, d = 4, 64
+    H = 4
     B, Sq, Sk = len(LENS_Q), max(LENS_Q), max(LENS_K)
     q, k, v, qmask, kmask, idx_q, idx_k, cu_q, cu_k = _batch(LENS_Q, LENS_K, H, d, dtype, seed=int(scale_mul * 8))
     tag = "bf16" if dtype == torch.bfloat16 else "f16"
@@ -56,7 +70,9 @@ def test_asm_forward_ragged_short_and_long_keys(impl, layout, dtype, scale_mul):
     nwg = (Sq + 255) // 256 * H * B
     ncu = torch.cuda.get_device_properties(DEV).multi_processor_count // 8 * 8
     persistent = impl == "ASM4P" or nwg > ncu
-    want = f"fa_fwd_d64p_{tag}_asm" if persistent else f"fa_fwd_d64_{tag}_asm"
+    want = f"fa_fwd_d{d}p_{tag}_asm" if persistent else f"fa_fwd_d{d}_{tag}_asm"
+    if d == 32:
+        want = "fa::fa_fwd_kernel<32,"      # head_dim <= 32: the HIP forward
     assert hip.fwd_kernel_name(B, H, d, Sq, Sk, dtype, impl=code) == want
     ctx = hip.force_impl(code) if impl != "AUTO" else contextlib.nullcontext()
     scale = d ** -0.5 * scale_mul
