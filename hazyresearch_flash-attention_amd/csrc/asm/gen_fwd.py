@@ -78,6 +78,8 @@ LAST_UNMASKED = True   # last tile: unmasked copy when every row sees the whole 
 MFMA_ZERO = True       # prologue: O, row sums, V buffer zeroed by MFMAs of a zero operand
 ORDET_ANDOR = True     # ORDET: the last P word enters the test by one v_and_or_b32 (mask in V_MTHR)
 PHASE_TAIL = 1         # ORDET test issued before the phase's last PHASE_TAIL MFMAs, its branch after them
+ORDET_BITOP3 = False   # ORDET: (T | P15) & M by one v_bitop3_b32 instead of v_and + v_and_or: one VALU fewer
+#                        per block and tile, measured 0.3-0.4 % SLOWER (profiles/r06/bitop3_ab.txt): A/B only
 
 
 def soff_walk():
@@ -545,6 +547,14 @@ class Gen:
                 op = 'v_or3_b32' if len(srcs) == 3 else 'v_or_b32'
                 steps.append((cvt_at[max(grp)] + 3, 3, V(f'{op} v{T}, ' + ', '.join(f'v{r}' for r in srcs), T, srcs)))
             end = cvt_at[last] + 3
+            if ORDET_BITOP3 and ORDET_ANDOR:
+                # (T | P15) & M in one v_bitop3_b32 (table 0xa8: S0 | S1, and S2), M = 0x40004000 in V_MTHR
+                end = cvt_at[15] + 3
+                M = V_MTHR[X]
+                steps.append((end, 3, Inst(f'v_bitop3_b32 v{T}, v{T}, v{P + 15}, v{M} bitop3:0xa8', 'valu', 4,
+                                           rd=[f'v{P + 15}', f'v{M}', f'v{T}'], wr=[f'v{T}'])))
+                steps.append((end + 2, 3, V(f'v_cmp_ne_u32 vcc, 0, v{T}', 'vcc', [T])))
+                return [x for _, _, x in sorted(steps, key=lambda z: (z[0], z[1]))]
             steps.append((end + 1, 3, V(f'v_and_b32 v{T}, 0x40004000, v{T}', T, [T])))
             if ORDET_ANDOR:
                 # the last P word joins after the mask: (P15 & M) | T, M = 0x40004000 in V_MTHR
@@ -2474,6 +2484,7 @@ def main():
     ap.add_argument('--shift', type=int, default=None, help='loop code placement: N 4-byte s_nop 0 after its alignment')
     ap.add_argument('--soff', type=int, default=None, help='DMA tiles by the SGPR offset of one descriptor (SOFF_WALK)')
     ap.add_argument('--carry', type=int, default=None, help="persistent: a block's decode carried from the previous block")
+    ap.add_argument('--bitop3', type=int, default=None, help='ORDET test: (T | P15) & M by one v_bitop3_b32')
     args = ap.parse_args()
     global LOOP_SHIFT, SOFF_WALK
     if args.shift is not None:
@@ -2483,6 +2494,9 @@ def main():
     global CARRY_DECODE
     if args.carry is not None:
         CARRY_DECODE = bool(args.carry)
+    global ORDET_BITOP3
+    if args.bitop3 is not None:
+        ORDET_BITOP3 = bool(args.bitop3)
     global DUMP
     if args.dump:
         pt, regs = args.dump.split(':')

@@ -550,6 +550,17 @@ class Sim:
             w.vcc = t > 0xFFFFFFFF
             self.vwrite(w, a[0], (t & 0xFFFFFFFF).astype(U))
             return
+        if op == 'v_bitop3_b32':
+            # D = BITOP3(S0, S1, S2, table): bit i of the table is the result for the source bits
+            # (S0 << 2) | (S1 << 1) | S2 = i (LLVM's encoding: (a | b) & c with S0 = a, S1 = b, S2 = c is 0xa8)
+            x0, x1, x2 = (self.vread(w, x) for x in a[1:4])
+            tbl = int(a[4].split(':')[1], 0)
+            r = np.zeros(64, dtype=U)
+            for i in range(8):
+                if tbl >> i & 1:
+                    r |= (x0 if i & 4 else ~x0) & (x1 if i & 2 else ~x1) & (x2 if i & 1 else ~x2)
+            self.vwrite(w, a[0], r.astype(U))
+            return
         src = [self.vread(w, x) for x in a[1:]]
         f = [s.view(np.float32) for s in src]
         with np.errstate(all='ignore'):
