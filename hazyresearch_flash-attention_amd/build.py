@@ -40,7 +40,9 @@ ASM_KERNELS = [("bf16", 64, 4, "fa_asm_fwd_d64_bf16"), ("f16", 64, 4, "fa_asm_fw
                ("bf16", 64, "p", "fa_asm_fwd_d64p_bf16"), ("f16", 64, "p", "fa_asm_fwd_d64p_f16"),
                ("bf16", 128, "p", "fa_asm_fwd_d128p_bf16"), ("f16", 128, "p", "fa_asm_fwd_d128p_f16"),
                ("bf16", 96, 4, "fa_asm_fwd_d96_bf16"), ("f16", 96, 4, "fa_asm_fwd_d96_f16"),
-               ("bf16", 96, "p", "fa_asm_fwd_d96p_bf16"), ("f16", 96, "p", "fa_asm_fwd_d96p_f16")]
+               ("bf16", 96, "p", "fa_asm_fwd_d96p_bf16"), ("f16", 96, "p", "fa_asm_fwd_d96p_f16"),
+               ("bf16", 32, 4, "fa_asm_fwd_d32_bf16"), ("f16", 32, 4, "fa_asm_fwd_d32_f16"),
+               ("bf16", 32, "p", "fa_asm_fwd_d32p_bf16"), ("f16", 32, "p", "fa_asm_fwd_d32p_f16")]
 LLVM_BIN = "/opt/rocm/lib/llvm/bin"
 # Per-source machine-scheduler choice, from one-process A/Bs of every LLVM AMDGPU strategy
 # (DESIGN 7.4): the forward kernels with the AMDGPU register-pressure trackers (north star +2 %,

@@ -43,6 +43,14 @@ extern const unsigned char fa_asm_fwd_d96p_bf16[];
 extern const unsigned long fa_asm_fwd_d96p_bf16_size;
 extern const unsigned char fa_asm_fwd_d96p_f16[];
 extern const unsigned long fa_asm_fwd_d96p_f16_size;
+extern const unsigned char fa_asm_fwd_d32_bf16[];
+extern const unsigned long fa_asm_fwd_d32_bf16_size;
+extern const unsigned char fa_asm_fwd_d32_f16[];
+extern const unsigned long fa_asm_fwd_d32_f16_size;
+extern const unsigned char fa_asm_fwd_d32p_bf16[];
+extern const unsigned long fa_asm_fwd_d32p_bf16_size;
+extern const unsigned char fa_asm_fwd_d32p_f16[];
+extern const unsigned long fa_asm_fwd_d32p_f16_size;
 }
 
 namespace fa {
@@ -90,10 +98,11 @@ constexpr int kMaxDev = 64;
 constexpr float kRescaleThr = 8.0f;   // fa_fwd_kernel.h RESCALE_THR
 
 // kernels: [form (0: D=64, 1: D=128, 2: D=64 persistent, 3: D=128 persistent, 4: D=96, 5: D=96
-// persistent) * 2 + dtype (0: bf16, 1: f16)]. The two-waves-per-SIMD form (gen_fwd.py --waves 8,
-// FA_IMPL_ASM8) measured even or slower in every A/B and left the library in
-// round 6; the generator keeps it for A/B builds.
-constexpr int kNumFns = 12;
+// persistent, 6: D=32, 7: D=32 persistent) * 2 + dtype (0: bf16, 1: f16)]. The two-waves-per-SIMD
+// form (gen_fwd.py --waves 8, FA_IMPL_ASM8) measured even or slower in every A/B
+// and left the library in round 6; the generator keeps it for A/B builds. The D=32 tile (head_dim
+// <= 32, zero-padded) joined in round 6, when it measured faster than the HIP D=32 forward.
+constexpr int kNumFns = 16;
 struct DevFns {
     hipModule_t mod[kNumFns] = {};
     hipFunction_t fn[kNumFns] = {};
@@ -117,13 +126,17 @@ hipError_t load_all(DevFns &d, int want) {
                                               fa_asm_fwd_d64p_bf16,  fa_asm_fwd_d64p_f16,
                                               fa_asm_fwd_d128p_bf16, fa_asm_fwd_d128p_f16,
                                               fa_asm_fwd_d96_bf16,   fa_asm_fwd_d96_f16,
-                                              fa_asm_fwd_d96p_bf16,  fa_asm_fwd_d96p_f16};
+                                              fa_asm_fwd_d96p_bf16,  fa_asm_fwd_d96p_f16,
+                                              fa_asm_fwd_d32_bf16,   fa_asm_fwd_d32_f16,
+                                              fa_asm_fwd_d32p_bf16,  fa_asm_fwd_d32p_f16};
     static const char *const names[kNumFns] = {"fa_fwd_d64_bf16_asm",   "fa_fwd_d64_f16_asm",
                                                "fa_fwd_d128_bf16_asm",  "fa_fwd_d128_f16_asm",
                                                "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
                                                "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm",
                                                "fa_fwd_d96_bf16_asm",   "fa_fwd_d96_f16_asm",
-                                               "fa_fwd_d96p_bf16_asm",  "fa_fwd_d96p_f16_asm"};
+                                               "fa_fwd_d96p_bf16_asm",  "fa_fwd_d96p_f16_asm",
+                                               "fa_fwd_d32_bf16_asm",   "fa_fwd_d32_f16_asm",
+                                               "fa_fwd_d32p_bf16_asm",  "fa_fwd_d32p_f16_asm"};
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     const bool exchanged = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
     hipError_t want_e = hipErrorNotFound;
@@ -175,11 +188,11 @@ uint32_t magic_half(uint32_t d) {   // ceil(2^32 / (2 d)) for d >= 1
 bool fwd_asm_eligible(const FaFwdArgs &a, const FaBlockMask &bm) {
     if (a.impl == FA_IMPL_HIP) return false;
     if (bm.mask || a.p_dropout > 0.f || a.rot_cos) return false;
-    // D = 64 tile: head_dim in (32, 64] (zero-padded); D = 128 tile: head_dim == 128 only (its Q loads
-    // and O stores address whole rows from one base); D = 96 tile (the D = 128 layout computing 96
-    // columns): head_dim 96, or 80 (k-step 5 of Q loaded as zeros, O columns 80..95 not stored)
-    if (!((a.head_dim > 32 && a.head_dim <= 64) || a.head_dim == 80 || a.head_dim == 96 || a.head_dim == 128))
-        return false;
+    // D = 32 tile: head_dim <= 32, D = 64 tile: head_dim in (32, 64] (both zero-padded); D = 128 tile:
+    // head_dim == 128 only (its Q loads and O stores address whole rows from one base); D = 96 tile (the
+    // D = 128 layout computing 96 columns): head_dim 96, or 80 (k-step 5 of Q loaded as zeros, O
+    // columns 80..95 not stored)
+    if (!(a.head_dim <= 64 || a.head_dim == 80 || a.head_dim == 96 || a.head_dim == 128)) return false;
     if (a.max_seqlen_q <= 0) return false;
     // byte strides must fit the kernel's 32-bit row strides; the magic divisions are exact for
     // n * d <= 2^30 (n < workgroups, d = q-blocks per head or heads)
@@ -232,8 +245,8 @@ static int persistent_grid_for(const FaFwdArgs &a, uint32_t nwg) {
 static int asm_form(const FaFwdArgs &a, int *pgrid) {
     const uint32_t nqb0 = (uint32_t)((a.max_seqlen_q + kRows - 1) / kRows);
     *pgrid = persistent_grid_for(a, nqb0 * (uint32_t)a.nheads * (uint32_t)a.batch);
-    const bool d128 = a.head_dim > 96, d96 = a.head_dim > 64 && !d128;
-    return *pgrid ? (d128 ? 3 : d96 ? 5 : 2) : (d128 ? 1 : d96 ? 4 : 0);
+    const bool d128 = a.head_dim > 96, d96 = a.head_dim > 64 && !d128, d32 = a.head_dim <= 32;
+    return *pgrid ? (d128 ? 3 : d96 ? 5 : d32 ? 7 : 2) : (d128 ? 1 : d96 ? 4 : d32 ? 6 : 0);
 }
 
 const char *asm_kernel_name(const FaFwdArgs &a) {
@@ -242,7 +255,9 @@ const char *asm_kernel_name(const FaFwdArgs &a) {
                                                "fa_fwd_d64p_bf16_asm",  "fa_fwd_d64p_f16_asm",
                                                "fa_fwd_d128p_bf16_asm", "fa_fwd_d128p_f16_asm",
                                                "fa_fwd_d96_bf16_asm",   "fa_fwd_d96_f16_asm",
-                                               "fa_fwd_d96p_bf16_asm",  "fa_fwd_d96p_f16_asm"};
+                                               "fa_fwd_d96p_bf16_asm",  "fa_fwd_d96p_f16_asm",
+                                               "fa_fwd_d32_bf16_asm",   "fa_fwd_d32_f16_asm",
+                                               "fa_fwd_d32p_bf16_asm",  "fa_fwd_d32p_f16_asm"};
     int pgrid = 0;
     return names[2 * asm_form(a, &pgrid) + (a.dtype == FA_DTYPE_BF16 ? 0 : 1)];
 }

@@ -135,6 +135,38 @@ def test_asm_form_forward_d96(form, d, causal, seqlen_q, seqlen_k):
         run_case("separate", 6, seqlen_q, seqlen_k, 8, d, torch.bfloat16, causal, 0.0, grad=False, seed=seqlen_k + d)
 
 
+@pytest.mark.parametrize("form", ["ASM4", "ASM4P"])
+@pytest.mark.parametrize("d", [8, 16, 24, 32])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("seqlen_q,seqlen_k", [(97, 97), (257, 513), (1025, 1100)])
+def test_asm_form_forward_d32(form, d, dtype, causal, seqlen_q, seqlen_k):
+    """The D = 32 tile (round 6: head_dim <= 32, zero-padded; one O d-block, 4-KiB K / V tiles, two
+    16-deep QK k-steps), one-block and persistent, against the fp32 oracle under the 2x rule."""
+    hip = _hip()
+    code = getattr(hip, f"FA_IMPL_{form}")
+    name = hip.fwd_kernel_name(6, 8, d, seqlen_q, seqlen_k, dtype, causal, impl=code)
+    assert name.startswith("fa_fwd_d32"), name
+    with hip.force_impl(code):
+        run_case("separate", 6, seqlen_q, seqlen_k, 8, d, dtype, causal, 0.0, grad=False, seed=seqlen_k + d)
+
+
+def test_d32_asm_and_hip_agree_at_the_d32_roofline_shape():
+    """B=8 H=12 S=2048 D=32 (the per-tile roofline shape): AUTO takes the assembly D = 32 tile
+    (persistent: 768 blocks), and its output is within one bf16 ulp-scale of the HIP forward's."""
+    from flash_attn import flash_attn_interface as fi
+    hip = _hip()
+    B, H, S, d = 8, 12, 2048, 32
+    assert hip.fwd_kernel_name(B, H, d, S, S, torch.bfloat16) == "fa_fwd_d32p_bf16_asm"
+    g = torch.Generator(device="cpu").manual_seed(1)
+    q, k, v = (torch.randn(B * S, H, d, generator=g).bfloat16().to(DEV) for _ in range(3))
+    cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=DEV)
+    out = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
+    with hip.force_impl(hip.FA_IMPL_HIP):
+        ref = fi.flash_attn_unpadded_func(q, k, v, cu, cu, S, S, 0.0)
+    assert (out.float() - ref.float()).abs().max().item() <= 1e-2
+
+
 @pytest.mark.parametrize("d", [64, 128])
 def test_asm_persistent_empty_key_set_after_tail(d):
     """the persistent form's .Lempty path right after a block that took the K/V tail

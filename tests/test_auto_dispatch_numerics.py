@@ -50,9 +50,8 @@ def test_asm_forward_ragged_short_and_long_keys(impl, layout, dtype, scale_mul):
 @pytest.mark.parametrize("scale_mul", [4.0, 0.25])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_non_default_scale_other_head_dims(d, scale_mul, dtype):
-    """a non-default softmax_scale at the other head-dim tiles (D = 32: the HIP
-    forward; D = 96 / 128: the assembly D = 96 / 128 tiles), the same ragged batch, forward and
-    backward. scale_mul is a power of two, so the oracle sees q rescaled exactly."""
+    """a non-default softmax_scale at the other head-dim tiles (the assembly D = 32,
+    96 and 128 tiles), the same ragged batch, forward and backward. scale_mul is a power of two, so the oracle sees q rescaled exactly."""
     _ragged_case("AUTO", "separate", dtype, scale_mul, d)
 
 
@@ -71,8 +70,6 @@ def _ragged_case(impl, layout, dtype, scale_mul, d):
     ncu = torch.cuda.get_device_properties(DEV).multi_processor_count // 8 * 8
     persistent = impl == "ASM4P" or nwg > ncu
     want = f"fa_fwd_d{d}p_{tag}_asm" if persistent else f"fa_fwd_d{d}_{tag}_asm"
-    if d == 32:
-        want = "fa::fa_fwd_kernel<32,"      # head_dim <= 32: the HIP forward
     assert hip.fwd_kernel_name(B, H, d, Sq, Sk, dtype, impl=code) == want
     ctx = hip.force_impl(code) if impl != "AUTO" else contextlib.nullcontext()
     scale = d ** -0.5 * scale_mul

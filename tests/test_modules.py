@@ -125,14 +125,24 @@ def test_flash_mha_module(rotary, padded, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("route", ["auto", "hip"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("D", [32, 64, 128])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-def test_fused_rotary_equals_separate_pass(causal, D, dtype):
+def test_fused_rotary_equals_separate_pass(route, causal, D, dtype):
     """FlashAttnRotaryQKVFunc gives the same output bits as rotating q and k first (fa_rotary) and
-    running the plain forward, whichever route it takes: D = 32 rotates q inside the HIP forward at
-    its Q load, D = 64 / 128 (assembly forward) rotates q and k in one fa_rotary pass; its backward
-    gives the same dk/dv bits and dq up to the order of the fp32 dQ atomics (D <= 64)."""
+    running the plain forward, whichever route it takes: AUTO (assembly forward at D = 32 / 64 / 128)
+    rotates q and k in one fa_rotary pass; under force_impl(FA_IMPL_HIP) the route follows the HIP
+    forward, which rotates q at its Q load (the route decision sees the forced impl); its
+    backward gives the same dk/dv bits and dq up to the order of the fp32 dQ atomics (D <= 64)."""
+    import contextlib
+    from flash_attn import flash_attn_hip as hip
+    ctx = hip.force_impl(hip.FA_IMPL_HIP) if route == "hip" else contextlib.nullcontext()
+    with ctx:
+        _fused_rotary_case(causal, D, dtype, route)
+
+
+def _fused_rotary_case(causal, D, dtype, route):
     from flash_attn.flash_attention import FlashAttnRotaryQKVFunc
     from flash_attn.flash_attn_interface import flash_attn_unpadded_qkvpacked_func
     from flash_attn.rotary import apply_rotary_emb_qkv_
@@ -148,8 +158,8 @@ def test_fused_rotary_equals_separate_pass(causal, D, dtype):
     rot = apply_rotary_emb_qkv_(b.clone(), cos, sin)
     cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device="cuda")
     from flash_attn import flash_attn_hip as hip
-    name = hip.fwd_kernel_name(B, H, D, S, S, dtype, causal, row_elems=3 * H * D)
-    assert name.endswith("_asm") == (D != 32), name
+    name = hip.fwd_kernel_name(B, H, D, S, S, dtype, causal, row_elems=3 * H * D, impl=hip._impl())
+    assert name.endswith("_asm") == (route == "auto"), name
     out_s = flash_attn_unpadded_qkvpacked_func(rot.reshape(B * S, 3, H, D), cu, S, 0.0, causal=causal)
     assert torch.equal(out_f.reshape(B * S, H, D), out_s)
     ga, = torch.autograd.grad(out_f, a, dout)
