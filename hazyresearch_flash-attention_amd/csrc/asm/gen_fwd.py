@@ -1382,8 +1382,22 @@ def sec(name):
     return Inst(name, 'sec', 0)
 
 
+PRO_ORDER = ('args', 'decode', 'decode_map', 'decode_wait', 'wave', 'state', 'soffinit', 'state2', 'lanes', 'rows',
+             'qload', 'dma', 'lanes_lds', 'lanes2', 'qscale', 'zero', 'start')
+
+
+PRO_ORDER_R5 = ('args', 'decode', 'decode_map', 'decode_wait', 'wave', 'state', 'soffinit', 'state2', 'lanes',
+                'lanes_lds', 'rows', 'lanes2', 'qload', 'dma', 'qscale', 'zero', 'start')   # round 5 (--proorder 0)
+PRO_ORDER_LANES_FIRST = ('args', 'decode', 'decode_map', 'wave', 'lanes', 'lanes_lds', 'decode_wait', 'state',
+                         'soffinit', 'state2', 'rows', 'lanes2', 'qload', 'dma', 'qscale', 'zero', 'start')  # --proorder 2
+
+
 def prologue(g):
-    return [x for x in prologue_sections(g) if x.kind != 'sec']
+    """The one-block prologue: its sections in PRO_ORDER (the per-lane address setup, which needs no
+    decoded value, between the decode's cu_seqlens loads and their first use)."""
+    sc = split_sections(prologue_sections(g))
+    assert set(sc) == set(PRO_ORDER), sorted(sc)
+    return sum((sc[k] for k in PRO_ORDER), [])
 
 
 def prologue_sections(g):
@@ -1441,8 +1455,12 @@ def prologue_sections(g):
           S('s_add_u32 s92, s50, s90'), S('s_addc_u32 s93, s51, 0'),
           Inst('s_load_dwordx2 s[76:77], s[92:93], 0x0', 'smem', 2, wr=['s76', 's77']),
           S('s_add_u32 s94, s52, s90'), S('s_addc_u32 s95, s53, 0'),
-          Inst('s_load_dwordx2 s[78:79], s[94:95], 0x0', 'smem', 2, wr=['s78', 's79']),
-          raw('s_waitcnt lgkmcnt(0)')]
+          Inst('s_load_dwordx2 s[78:79], s[94:95], 0x0', 'smem', 2, wr=['s78', 's79'])]
+    # the cu_seqlens loads' wait is a section of its own: the one-block prologue (prologue(), PRO_ORDER)
+    # runs the per-lane address setup between the loads and this wait (the SALU helper S() does not
+    # list its registers, so the hazard pass cannot place it); the persistent decodes add it after
+    # every copy of decode_map
+    p += [sec('decode_wait'), raw('s_waitcnt lgkmcnt(0)')]
     p.append(sec('wave'))
     if WAVE_MODE != 'early':
         p += wave_id_insts()
@@ -1489,6 +1507,27 @@ def prologue_sections(g):
     p += [V(f'v_and_b32 v{L}, 63, v0', L, [0]), V('v_and_b32 v16, 31, v0', 16, [0]),
           V('v_bfe_u32 v17, v0, 5, 1', 17, [0]), V('v_bfe_u32 v18, v0, 2, 2', 18, [0]),
           V('v_and_b32 v19, 3, v0', 19, [0]), V('v_bfe_u32 v20, v0, 4, 1', 20, [0])]
+    p += [V(f'v_mov_b32 v{V_NEGINF}, 0xff800000', V_NEGINF, []), V(f'v_mov_b32 v{V_ONEF}, 1.0', V_ONEF, []),
+          V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
+    # DMA source offsets: pieces `wave + 4i` of a tile; lane l -> row RPP p + l/LPR, slot l%LPR
+    # (RPP = rows per 1-KiB piece, LPR = 16-B chunks per row)
+    lpr = D // 8
+    rpp = 1024 // ROWB
+    p += [V(f'v_lshrrev_b32 v33, {lpr.bit_length() - 1}, v{L}', 33, [L]), V(f'v_and_b32 v34, {lpr - 1}, v{L}', 34, [L]),
+          S(f's_lshl_b32 s97, s{S_WAVE}, {rpp.bit_length() - 1}')]
+    for i in range(NP):
+        p += [S(f's_add_u32 s96, s97, {NWAVES * rpp * i}'), V('v_add_u32 v35, s96, v33', 35, [33])]
+        p += xfun(36, 35, 37, 38)
+        p += [V('v_xor_b32 v36, v34, v36', 36, [34, 36]), V('v_lshlrev_b32 v37, 3, v36', 37, [36]),
+              V('v_cmp_gt_u32 vcc, s74, v37', 'vcc', [37]),
+              V('v_mul_lo_u32 v38, v35, s63', 38, [35]), V('v_lshl_add_u32 v38, v36, 4, v38', 38, [36, 38]),
+              Inst(f'v_cndmask_b32 v{V_DMA + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'], wr=[f'v{V_DMA + i}']),
+              V('v_mul_lo_u32 v38, v35, s64', 38, [35]), V('v_lshl_add_u32 v38, v36, 4, v38', 38, [36, 38]),
+              Inst(f'v_cndmask_b32 v{V_DMA + NP + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'],
+                   wr=[f'v{V_DMA + NP + i}'])]
+    # K / V^T fragment read addresses (LDS), needed from the first LDS reads on: own section, so that a
+    # prologue order may issue the Q loads and first DMAs before it (PRO_ORDER)
+    p.append(sec('lanes_lds'))
     p += xfun(21, 16, 22, 23)
     rsh = ROWB.bit_length() - 1     # log2 of the LDS row bytes
     for ks in range(NKS):   # K fragment reads: row l32, chunk 2ks + hi
@@ -1506,24 +1545,6 @@ def prologue_sections(g):
                   V(f'v_lshl_add_u32 v{V_VADDR + dt * 2 + half}, v27, {rsh}, v29', V_VADDR + dt * 2 + half, [27, 29]),
                   V(f'v_add_u32 v{V_VADDR + dt * 2 + half}, {VREG}, v{V_VADDR + dt * 2 + half}',
                     V_VADDR + dt * 2 + half, [V_VADDR + dt * 2 + half])]
-    p += [V(f'v_mov_b32 v{V_NEGINF}, 0xff800000', V_NEGINF, []), V(f'v_mov_b32 v{V_ONEF}, 1.0', V_ONEF, []),
-          V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
-    # DMA source offsets: pieces `wave + 4i` of a tile; lane l -> row RPP p + l/LPR, slot l%LPR
-    # (RPP = rows per 1-KiB piece, LPR = 16-B chunks per row)
-    lpr = D // 8
-    rpp = 1024 // ROWB
-    p += [V(f'v_lshrrev_b32 v33, {lpr.bit_length() - 1}, v{L}', 33, [L]), V(f'v_and_b32 v34, {lpr - 1}, v{L}', 34, [L]),
-          S(f's_lshl_b32 s91, s{S_WAVE}, {rpp.bit_length() - 1}')]
-    for i in range(NP):
-        p += [S(f's_add_u32 s92, s91, {NWAVES * rpp * i}'), V('v_add_u32 v35, s92, v33', 35, [33])]
-        p += xfun(36, 35, 37, 38)
-        p += [V('v_xor_b32 v36, v34, v36', 36, [34, 36]), V('v_lshlrev_b32 v37, 3, v36', 37, [36]),
-              V('v_cmp_gt_u32 vcc, s74, v37', 'vcc', [37]),
-              V('v_mul_lo_u32 v38, v35, s63', 38, [35]), V('v_lshl_add_u32 v38, v36, 4, v38', 38, [36, 38]),
-              Inst(f'v_cndmask_b32 v{V_DMA + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'], wr=[f'v{V_DMA + i}']),
-              V('v_mul_lo_u32 v38, v35, s64', 38, [35]), V('v_lshl_add_u32 v38, v36, 4, v38', 38, [36, 38]),
-              Inst(f'v_cndmask_b32 v{V_DMA + NP + i}, v31, v38, vcc', 'valu', rd=['v31', 'v38', 'vcc'],
-                   wr=[f'v{V_DMA + NP + i}'])]
     # Q load offsets (v43..v50), O store offsets, LSE offsets of blocks A (rows +0) and B (+32)
     p.append(sec('rows'))
     p += [S(f's_lshl_b32 s93, s{S_WAVE}, {(32 * len(BLOCKS)).bit_length() - 1}'), S('s_add_u32 s93, s93, s90')]
@@ -1812,18 +1833,18 @@ def prologue_persist(g):
                           raw('s_waitcnt lgkmcnt(0)'),
                           S('s_mov_b32 s99, s2'), S('s_mov_b32 s101, 0'), S('s_mov_b32 s98, 0'),
                           V(f'v_mov_b32 v{V_TID}, v0', V_TID, [0])]
-    pro_a += sc['wave'] + sc['lanes'] + sc['lanes2']
+    pro_a += sc['wave'] + sc['lanes'] + sc['lanes_lds'] + sc['lanes2']
     # next block (clamped to the last one: its decode stays in range) -> Q descriptor s[4:7], q-block s3
     nxt = [S('s_add_u32 s80, s99, s100'), S('s_sub_u32 s81, s71, 1'), S('s_min_u32 s80, s80, s81')]
-    nxt += sc['decode_map']
+    nxt += sc['decode_map'] + [raw('s_waitcnt lgkmcnt(0)')]
     nxt += [S('s_sub_u32 s77, s77, s76'), S(f's_mov_b32 s{S_NQB}, s87'),
             S('s_mov_b32 s0, s78'), S('s_sub_u32 s1, s79, s78'), S('s_mov_b32 s2, s89')]
     nxt += make_desc(S_NQD, 40, 76, 62, 54, 55, 77)
     lanes_t = [V(f'v_and_b32 v16, 31, v{V_TID}', 16, [V_TID]), V(f'v_bfe_u32 v17, v{V_TID}, 5, 1', 17, [V_TID]),
                V('v_mov_b32 v31, 0x80000000', 31, []), V('v_mov_b32 v32, 0', 32, [])]
-    dec2 = [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
+    dec2 = [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + [raw('s_waitcnt lgkmcnt(0)')]
     if 'dec3' in PROBE:     # timing probe: the current block's decode twice (the price of one decode)
-        dec2 = dec2 + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']]
+        dec2 = dec2 + [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + [raw('s_waitcnt lgkmcnt(0)')]
     if carry_decode():
         # the block's sequence bounds and (b, h, q-block) come from the previous decode of this block
         # (the previous block's `nxt`, or for a workgroup's first block pro_a, or the .Lend path): no
@@ -1832,8 +1853,10 @@ def prologue_persist(g):
                    S('s_add_u32 s79, s0, s1'), S(f's_mov_b32 s87, s{S_NQB}'), S('s_mov_b32 s88, s86'),
                    S('s_mov_b32 s89, s2')]
         if 'dec3' in PROBE:     # timing probe: one more decode of this block (the price of a decode)
-            restore = [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + restore
-        pro_a += [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + carry_save()
+            restore = [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + \
+                [raw('s_waitcnt lgkmcnt(0)')] + restore
+        pro_a += [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + \
+            [raw('s_waitcnt lgkmcnt(0)')] + carry_save()
         pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + restore + sc['state'] + sc['state2'] + lanes_t + sc['rows'] + \
             nxt + carry_save(after_nxt=True) + sc['soffinit'] + pstamp(PS_V + 4, 'pstA') + \
             ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
@@ -2275,7 +2298,8 @@ def build(g):
         if carry_decode():
             # a q-block past its sequence skipped `nxt`: decode the next block here
             lend_dec = [S('s_add_u32 s80, s99, s100'), S('s_sub_u32 s81, s71, 1'), S('s_min_u32 s80, s80, s81')] + \
-                [x for x in split_sections(prologue_sections(g))['decode_map']] + carry_save()
+                [x for x in split_sections(prologue_sections(g))['decode_map']] + [raw('s_waitcnt lgkmcnt(0)')] + \
+                carry_save()
         end = [label('.Lend'), S(f's_mov_b32 s{S_QPF}, 0')] + lend_dec + [label('.Lseam')] + pstamp_store() + [
                S(f's_add_u32 s{S_L}, s{S_L}, s{S_G}'), S(f's_cmp_ge_u32 s{S_L}, s71'), raw('s_cbranch_scc1 .Ldone'),
                raw('s_barrier'), raw('s_branch .Lblock')]
@@ -2485,6 +2509,7 @@ def main():
     ap.add_argument('--soff', type=int, default=None, help='DMA tiles by the SGPR offset of one descriptor (SOFF_WALK)')
     ap.add_argument('--carry', type=int, default=None, help="persistent: a block's decode carried from the previous block")
     ap.add_argument('--bitop3', type=int, default=None, help='ORDET test: (T | P15) & M by one v_bitop3_b32')
+    ap.add_argument('--proorder', type=int, default=None, help='one-block prologue: 0 = round-5 section order')
     args = ap.parse_args()
     global LOOP_SHIFT, SOFF_WALK
     if args.shift is not None:
@@ -2497,6 +2522,9 @@ def main():
     global ORDET_BITOP3
     if args.bitop3 is not None:
         ORDET_BITOP3 = bool(args.bitop3)
+    global PRO_ORDER
+    if args.proorder is not None:
+        PRO_ORDER = {0: PRO_ORDER_R5, 1: PRO_ORDER, 2: PRO_ORDER_LANES_FIRST}[args.proorder]
     global DUMP
     if args.dump:
         pt, regs = args.dump.split(':')
