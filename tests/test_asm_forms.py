@@ -201,3 +201,46 @@ def test_asm_persistent_empty_key_set_after_tail(d):
         pt, _ = attention_ref(q[qs][None], k[ks][None], v[ks][None], upcast=False, reorder_ops=True)
         err = (out[qs].float() - ref[0].float()).abs().max().item()
         assert err <= max_err_bound(pt, ref, floor=ulp_floor(ref)), (b, err)
+
+
+@pytest.mark.parametrize("form", ["ASM4", "ASM4P"])
+@pytest.mark.parametrize("d", [32, 64])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("spike", [False, True])
+def test_asm_forward_probabilities_through_one_hot_v(form, d, causal, spike):
+    """the assembly forward's own P, observed directly. With V's rows one-hot
+    (key k of chunk j -> column k - d j, zero rows outside the chunk), O = P V / l is the normalised
+    probability of every key of chunk j, computed by the kernel's exps, its rounded P and its MFMA row
+    sums; compared with softmax(scale Q K^T) in fp32 over every chunk, within the rounding of P to
+    bf16 and of O to bf16 (2^-7 relative + 1e-3). spike: a key that passes the running max in a later
+    tile (the out-of-line rescale path)."""
+    from flash_attn import flash_attn_interface as fi
+    hip = _hip()
+    B, H, Sq, Sk = 2, 2, 300, 200
+    g = torch.Generator(device="cpu").manual_seed(d + 7 * causal + 3 * spike)
+    q = torch.randn(B * Sq, H, d, generator=g).bfloat16()
+    k = torch.randn(B * Sk, H, d, generator=g).bfloat16()
+    if spike:
+        k[150] = (q[7].float() * 3.0).bfloat16()        # sequence 0, tile 2, strong for query 7
+    q, k = q.to(DEV), k.to(DEV)
+    cu_q = torch.arange(0, (B + 1) * Sq, Sq, dtype=torch.int32, device=DEV)
+    cu_k = torch.arange(0, (B + 1) * Sk, Sk, dtype=torch.int32, device=DEV)
+    code = getattr(hip, f"FA_IMPL_{form}")
+    assert hip.fwd_kernel_name(B, H, d, Sq, Sk, torch.bfloat16, causal, impl=code).endswith("_asm")
+    qf, kf = q.float().view(B, Sq, H, d), k.float().view(B, Sk, H, d)
+    s = torch.einsum("bqhd,bkhd->bhqk", qf, kf) * d ** -0.5
+    if causal:
+        s = s.masked_fill(torch.triu(torch.ones(Sq, Sk, dtype=torch.bool, device=DEV), 1), float("-inf"))
+    p_ref = torch.softmax(s, -1)                                   # (B, H, Sq, Sk)
+    for j in range((Sk + d - 1) // d):
+        keys = torch.arange(Sk, device=DEV)
+        v = torch.zeros(B, Sk, H, d, device=DEV)
+        inc = (keys >= j * d) & (keys < (j + 1) * d)
+        v[:, inc, :, :] = torch.eye(d, device=DEV)[keys[inc] - j * d][None, :, None, :]
+        v = v.bfloat16().view(B * Sk, H, d)
+        with hip.force_impl(code):
+            out = fi.flash_attn_unpadded_func(q, k, v, cu_q, cu_k, Sq, Sk, 0.0, causal=causal)
+        got = out.float().view(B, Sq, H, d).permute(0, 2, 1, 3)[..., :int(inc.sum())]
+        want = p_ref[..., j * d:j * d + int(inc.sum())]
+        bad = (got - want).abs() > 2 ** -7 * want.abs() + 1e-3
+        assert not bad.any(), (j, (got - want).abs().max().item())
