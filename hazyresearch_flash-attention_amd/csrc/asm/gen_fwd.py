@@ -1857,10 +1857,24 @@ def prologue_persist(g):
                 [raw('s_waitcnt lgkmcnt(0)')] + restore
         pro_a += [S('s_mov_b32 s80, s99')] + [copy.copy(x) for x in sc['decode_map']] + \
             [raw('s_waitcnt lgkmcnt(0)')] + carry_save()
-        pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + restore + sc['state'] + sc['state2'] + lanes_t + sc['rows'] + \
-            nxt + carry_save(after_nxt=True) + sc['soffinit'] + pstamp(PS_V + 4, 'pstA') + \
-            ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
-    else:
+        if DMA_FIRST:
+            # the block's first DMAs go out before the next block's decode (pb2): its cu_seqlens
+            # round trip runs under their latency. The decode's temporaries include the DMA offsets
+            # s80..s83, which a VGPR lane stash keeps across it.
+            pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + restore + sc['state'] + sc['state2'] + lanes_t + \
+                sc['rows'] + sc['soffinit'] + pstamp(PS_V + 4, 'pstA') + \
+                ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
+            stash = [Inst(f'v_writelane_b32 v{V_STASH}, s{80 + i}, {i}', 'valu', rd=[f's{80 + i}'], wr=[f'v{V_STASH}'])
+                     for i in range(4)]
+            unstash = [Inst(f'v_readlane_b32 s{80 + i}, v{V_STASH}, {i}', 'rfl', rd=[f'v{V_STASH}'], wr=[f's{80 + i}'])
+                       for i in range(4)]
+            nxt_late = stash + nxt + carry_save(after_nxt=True) + unstash
+        else:
+            pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + restore + sc['state'] + sc['state2'] + lanes_t + \
+                sc['rows'] + nxt + carry_save(after_nxt=True) + sc['soffinit'] + pstamp(PS_V + 4, 'pstA') + \
+                ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
+    nxt_late = nxt_late if carry_decode() and DMA_FIRST else []
+    if not carry_decode():
         pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + nxt + dec2 + \
             sc['state'] + sc['soffinit'] + sc['state2'] + lanes_t + \
             sc['rows'] + pstamp(PS_V + 4, 'pstA') + ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
@@ -1928,7 +1942,7 @@ def prologue_persist(g):
     # the first block of every workgroup never wrote it: the negative round-0 prologues of
     # profiles/r04_pstamps/pstamps_r04f/h.)
     pb2 = [label('.Lqdone')] + pstamp(PS_V + 4, 'pstB') + [S('s_cmp_eq_u32 s101, 2'), raw('s_cbranch_scc1 .Lkvpf')] + \
-        sc['dma'] + qs + pf + \
+        sc['dma'] + nxt_late + qs + pf + \
         sc['zero'] + start_with_wait(start_pieces() + nq)
     if qcb is not None:
         # pb2 as [head up to the branch, the copy, the first-block scale, the rest from .Lqsdone]
@@ -1947,6 +1961,8 @@ def prologue_persist(g):
 
 N_STORES = 10         # LSE + O stores per wave of the epilogue (D = 64: 2 x (1 + 4); set_persist)
 CARRY_DECODE = True   # persistent form: a block's decode carried from the previous block's next-block decode
+DMA_FIRST = True      # persistent carry form: the block's first DMAs before the next block's decode
+V_STASH = 209         # DMA_FIRST: lanes 0..3 keep the SGPR DMA offsets s80..s83 across the decode
 
 
 def carry_decode():
@@ -2510,6 +2526,7 @@ def main():
     ap.add_argument('--carry', type=int, default=None, help="persistent: a block's decode carried from the previous block")
     ap.add_argument('--bitop3', type=int, default=None, help='ORDET test: (T | P15) & M by one v_bitop3_b32')
     ap.add_argument('--proorder', type=int, default=None, help='one-block prologue: 0 = round-5 section order')
+    ap.add_argument('--dmafirst', type=int, default=None, help="persistent: the block's first DMAs before the next decode")
     args = ap.parse_args()
     global LOOP_SHIFT, SOFF_WALK
     if args.shift is not None:
@@ -2522,6 +2539,9 @@ def main():
     global ORDET_BITOP3
     if args.bitop3 is not None:
         ORDET_BITOP3 = bool(args.bitop3)
+    global DMA_FIRST
+    if args.dmafirst is not None:
+        DMA_FIRST = bool(args.dmafirst)
     global PRO_ORDER
     if args.proorder is not None:
         PRO_ORDER = {0: PRO_ORDER_R5, 1: PRO_ORDER, 2: PRO_ORDER_LANES_FIRST}[args.proorder]

@@ -493,6 +493,14 @@ class Sim:
         if op == 'v_readfirstlane_b32':
             self.swrite(w, a[0], int(self.vread(w, a[1])[0]))
             return
+        if op == 'v_readlane_b32':
+            self.swrite(w, a[0], int(self.vread(w, a[1])[self.sread(w, a[2]) & 63]))
+            return
+        if op == 'v_writelane_b32':
+            d = self.vread(w, a[0])
+            d[self.sread(w, a[2]) & 63] = self.sread(w, a[1])
+            self.vwrite(w, a[0], d)
+            return
         if op.startswith('v_cmp_'):
             kind = op[6:]
             if kind.endswith('_e32'):
