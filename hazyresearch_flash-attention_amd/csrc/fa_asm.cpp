@@ -5,7 +5,7 @@
 // loaded per device on first use with hipModuleLoadData and launched with hipModuleLaunchKernel
 // on the caller's stream (so it is captured into hipGraphs like the HIP kernels).
 //
-// It serves head_dim in (32, 64] (the D=64 tile), 80 and 96 (the D=96 tile: the D=128 layout computing
+// It serves head_dim <= 32 (the D=32 tile, round 6), (32, 64] (the D=64 tile), 80 and 96 (the D=96 tile: the D=128 layout computing
 // 96 columns) and 128 (the D=128 tile), fp16/bf16, causal or not, no dropout, dense (no block mask), no
 // fused rotary. Everything else keeps the HIP kernels of fa_fwd_kernel.h. Semantics are the same: var-len sequences through cu_seqlens,
 // rows past a sequence neither read nor written, LSE = m*scale + ln(sum) (-inf for no keys).

@@ -75,7 +75,7 @@ class FlashAttnRotaryQKVFunc:
 class _FlashAttnRotaryQKVFuncPy(torch.autograd.Function):
     """Attention over a padded, contiguous qkv (B, S, 3, H, D) with rotary embeddings fused into
     the forward (README.md:56 "Fuse rotary embedding"; rotation = rotary.py:31-41):
-    * forward: where fa_fwd takes an assembly kernel (no dropout, head_dim in (32, 64], 80, 96, 128)
+    * forward: where fa_fwd takes an assembly kernel (no dropout, head_dim <= 64, 80, 96, 128)
       one fa_rotary pass rotates q and k into a (B, S, 2, H, D) buffer and the assembly forward reads
       it (measured faster than the HIP forward rotating q at its load); otherwise k
       is rotated by one fa_rotary pass into a (B, S, H, D) buffer (the backward needs it anyway) and

@@ -21,7 +21,7 @@
  *   fa_rotary               <- apply_rotary_pos_emb + RotaryEmbedding(2D).forward and their autograd
  *                              backward (flash_attn/rotary.py:22-41, 86-135)
  *   (fa_fwd runs hand-scheduled gfx950 assembly kernels, csrc/asm/gen_fwd.py, embedded in the library
- *    as code objects, for head_dim in (32, 64], 80, 96 or 128, fp16/bf16, causal or not, no dropout, dense,
+ *    as code objects, for head_dim ≤ 64 (≤ 32: the D = 32 tile), 80, 96 or 128, fp16/bf16, causal or not, no dropout, dense,
  *    no fused rotary; the persistent form for non-causal grids with more blocks than CUs; every form
  *    computes fp32-exact scores; fa_asm.cpp fwd_asm_eligible / persistent_grid_for).
  *    FaFwdArgs.impl selects a form or the HIP kernels.)
@@ -107,7 +107,7 @@ typedef struct FaFwdArgs {
     const void *rot_sin;
     int64_t rot_stride;
     /* Kernel family (FA_IMPL_*). FA_IMPL_AUTO picks the fastest kernel for the shape: the
-     * hand-scheduled assembly forward for head_dim in (32, 64], 80, 96 or 128, fp16/bf16, no dropout,
+     * hand-scheduled assembly forward for head_dim ≤ 64 (≤ 32: the D = 32 tile), 80, 96 or 128, fp16/bf16, no dropout,
      * dense, no fused rotary (non-causal grids with more blocks than CUs take its persistent form); the
      * HIP kernels otherwise. FA_IMPL_HIP forces the HIP kernels; FA_IMPL_ASM4 / FA_IMPL_ASM4P force
      * the one-wave-per-SIMD assembly form, one workgroup per block or persistent, where the shape is
