@@ -1864,6 +1864,7 @@ def prologue_persist(g):
             pb1 = [label('.Lblock')] + pstamp(PS_V + 2) + restore + sc['state'] + sc['state2'] + lanes_t + \
                 sc['rows'] + sc['soffinit'] + pstamp(PS_V + 4, 'pstA') + \
                 ([S('s_cmp_eq_u32 s101, 0'), raw('s_cbranch_scc1 .Lqload')] if PERSIST_Q else [])
+            assert V_TID < V_STASH < NVGPR_PERSIST <= NVGPR, 'V_STASH: a spare VGPR of the persistent map'
             stash = [Inst(f'v_writelane_b32 v{V_STASH}, s{80 + i}, {i}', 'valu', rd=[f's{80 + i}'], wr=[f'v{V_STASH}'])
                      for i in range(4)]
             unstash = [Inst(f'v_readlane_b32 s{80 + i}, v{V_STASH}, {i}', 'rfl', rd=[f'v{V_STASH}'], wr=[f's{80 + i}'])
