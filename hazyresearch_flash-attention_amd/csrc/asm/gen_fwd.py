@@ -1619,7 +1619,7 @@ def prologue_sections(g):
               for X in BLOCKS for r in range(4 * NKS)] if not QL_VGPR else []
     if 'nopro' not in PROBE:
         p += g.dma('K', 0)
-        for t in range(DIST):
+        for t in range(DIST - (1 if defer_dma() else 0)):
             p += g.dma('K', t + 1) + g.dma('V', t)
     # zero O, row sums, the V fragment buffer PV_B(-1) reads and P_B (PV_B(-1) of tile 0 adds
     # nothing); m = -inf
@@ -1672,6 +1672,9 @@ def prologue_sections(g):
     # (8 waves: phase 0 reads K2 as well: K0 K1 V0 K2 landed, all but the 3 youngest pieces)
     p += [raw(f's_waitcnt vmcnt({3 if NWAVES == 8 else start_pieces()})')]
     p += [raw('s_barrier')]
+    if defer_dma() and 'nopro' not in PROBE:
+        # DEFER_DMA: the prologue's last DMA tile (K(DIST), V(DIST-1)) goes out after the barrier
+        p += g.dma('K', DIST) + g.dma('V', DIST - 1)
     p += stamp(STAMP_V + 12) if 'stamps' in PROBE else []
     p += pstamp(PS_V + 4)
     # every wave reads K0 before any wave passes the next barrier when the loop's first DMA into K0's
@@ -2139,8 +2142,19 @@ def bar2_vmcnt():
 
 def start_pieces():
     """DMA pieces that may still be in flight at the prologue's barrier: pieces_wait(), or with
-    BAR2 one tile fewer (no barrier after tile 0: tile 1's K(2), V(1) must be published here)."""
-    return pieces_wait() - (min(2 * NP, 4) if BAR2 else 0)
+    BAR2 one tile fewer (no barrier after tile 0: tile 1's K(2), V(1) must be published here);
+    DEFER_DMA: the last prologue tile is not issued yet."""
+    n = pieces_wait() - (min(2 * NP, 4) if BAR2 else 0)
+    return n - 2 * NP if defer_dma() else n
+
+
+DEFER_DMA = True      # 4 waves, D <= 64: the prologue's last DMA tile after its barrier
+
+
+def defer_dma():
+    """DEFER_DMA applies where the prologue's barrier already waits for every earlier piece: the
+    4-wave D <= 64 forms (BAR2, ring 6, distance 3: start_pieces() is exactly that tile's pieces)."""
+    return DEFER_DMA and NWAVES == 4 and D <= 64 and BAR2 and pieces_wait() - min(2 * NP, 4) == 2 * NP
 
 
 def pieces_wait():
@@ -2527,6 +2541,7 @@ def main():
     ap.add_argument('--carry', type=int, default=None, help="persistent: a block's decode carried from the previous block")
     ap.add_argument('--bitop3', type=int, default=None, help='ORDET test: (T | P15) & M by one v_bitop3_b32')
     ap.add_argument('--proorder', type=int, default=None, help='one-block prologue: 0 = round-5 section order')
+    ap.add_argument('--defer', type=int, default=None, help="prologue: the last DMA tile after the barrier")
     ap.add_argument('--dmafirst', type=int, default=None, help="persistent: the block's first DMAs before the next decode")
     args = ap.parse_args()
     global LOOP_SHIFT, SOFF_WALK
@@ -2540,6 +2555,9 @@ def main():
     global ORDET_BITOP3
     if args.bitop3 is not None:
         ORDET_BITOP3 = bool(args.bitop3)
+    global DEFER_DMA
+    if args.defer is not None:
+        DEFER_DMA = bool(args.defer)
     global DMA_FIRST
     if args.dmafirst is not None:
         DMA_FIRST = bool(args.dmafirst)
