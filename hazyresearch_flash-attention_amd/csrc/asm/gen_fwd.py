@@ -60,7 +60,9 @@ DMA_P2 = False         # all four DMA pieces of a tile in phase 2 (K's with V's)
 SPEC = True            # exps against the current max; rescale test branches at the phase end
 ORDET = True           # rescale test = top exponent bit of the packed P (any P >= 2) by an OR tree;
 #                        the max tree moves into the out-of-line rescale block
-ORDET_DELTA = {'bf16': 8.0, 'f16': 2.0}   # a rescale sets m = tile max * c + delta (P <= 2^-delta)
+ORDET_DELTA = {'bf16': 8.0, 'f16': 4.0}   # a rescale sets m = tile max * c + delta (P <= 2^-delta)
+# (f16: P's smallest normal is 2^-14, so a larger delta turns more of a row's small weights subnormal; 4
+# instead of round 3's 2 measured C2 -10 % (fewer rescales) at unchanged fp16 errors: DESIGN.md 4.0d)
 EXP_LAG = 4            # exp_stream: fma(i) -> exp(i) distance (instructions)
 CVT_LAG = 4            # exp_stream: exp -> cvt distance
 MC_BANKS = False       # fma reads m*c from one of 4 copies in a VGPR bank other than its S operand
@@ -2541,6 +2543,7 @@ def main():
     ap.add_argument('--carry', type=int, default=None, help="persistent: a block's decode carried from the previous block")
     ap.add_argument('--bitop3', type=int, default=None, help='ORDET test: (T | P15) & M by one v_bitop3_b32')
     ap.add_argument('--proorder', type=int, default=None, help='one-block prologue: 0 = round-5 section order')
+    ap.add_argument('--fdelta', type=float, default=None, help='f16: the rescale delta (P <= 2^-delta after a rescale)')
     ap.add_argument('--defer', type=int, default=None, help="prologue: the last DMA tile after the barrier")
     ap.add_argument('--dmafirst', type=int, default=None, help="persistent: the block's first DMAs before the next decode")
     args = ap.parse_args()
@@ -2555,6 +2558,8 @@ def main():
     global ORDET_BITOP3
     if args.bitop3 is not None:
         ORDET_BITOP3 = bool(args.bitop3)
+    if args.fdelta is not None:
+        ORDET_DELTA['f16'] = args.fdelta
     global DEFER_DMA
     if args.defer is not None:
         DEFER_DMA = bool(args.defer)

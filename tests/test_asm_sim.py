@@ -194,7 +194,7 @@ def test_generated_kernel_assembles(dtype, hd, waves, persist, tmp_path):
     ([130], [200], False, "bf16"),            # 3 full tiles + a masked one, rows past the block end
     ([257, 40], [33, 190], False, "bf16"),    # var-len, two q-blocks, single masked tile
     ([70], [700], False, "bf16"),             # 11 tiles: every unrolled loop position and its last-tile exit
-    ([70], [700], False, "f16"),              # (fp16: the rescale delta of 2, frequent rescales)
+    ([70], [700], False, "f16"),              # (fp16: its own rescale delta)
     ([40, 64], [0, 65], False, "bf16"),       # empty key set (zeros, -inf)
     ([300], [300], True, "bf16"),             # causal: the diagonal band of two q-blocks
 ])
@@ -249,7 +249,7 @@ def test_asm_forward_d32_causal_and_persistent_in_simulator():
 
 @pytest.mark.parametrize("lens_q,lens_k,H,D,grid,dtype,causal,scale", [
     ([130], [200], 1, 64, None, "bf16", False, None),       # one-block form: 3 full tiles + a masked one
-    ([70], [700], 1, 64, None, "f16", False, None),         # 11 tiles, fp16 (rescale delta 2)
+    ([70], [700], 1, 64, None, "f16", False, None),         # 11 tiles, fp16 (its own rescale delta)
     ([40, 64], [0, 65], 1, 48, None, "bf16", False, None),  # empty key set, head_dim < 64
     ([300], [300], 1, 64, None, "bf16", True, None),        # causal band
     ([70], [300], 1, 64, None, "bf16", False, 3.0),         # forced rescales past tile 0

@@ -1,5 +1,5 @@
 """Forward error against an fp64 reference for the library FA_HIP_LIB names (tools only): the
-signed mean and max of the LSE error and the O error, bf16, non-causal and causal, at a few shapes.
+signed mean and max of the LSE error and the O error, bf16 or fp16, non-causal and causal, at a few shapes.
 Compares the rounding of P between library builds (e.g. PTRUNC's truncation + delta shift against the
 round-to-nearest conversion).
 
@@ -19,14 +19,17 @@ from flash_attn import flash_attn_hip as hip  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="prod")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     a = ap.parse_args()
+    dt = torch.float16 if a.dtype == "fp16" else torch.bfloat16
     dev = torch.device("cuda")
     for (B, H, S, D, causal, scale_mul) in ((2, 4, 2048, 64, False, 1.0), (2, 4, 2048, 64, True, 1.0),
-                                          (4, 4, 512, 32, False, 1.0), (2, 4, 1024, 64, False, 4.0)):
+                                          (4, 4, 512, 32, False, 1.0), (2, 4, 1024, 64, False, 4.0),
+                                          (1, 4, 8192, 64, False, 1.0), (1, 4, 8192, 64, False, 0.25)):
         g = torch.Generator(device=dev).manual_seed(1)
-        q = torch.randn(B * S, H, D, generator=g, device=dev).to(torch.bfloat16)
-        k = torch.randn(B * S, H, D, generator=g, device=dev).to(torch.bfloat16)
-        v = torch.randn(B * S, H, D, generator=g, device=dev).to(torch.bfloat16)
+        q = torch.randn(B * S, H, D, generator=g, device=dev).to(dt)
+        k = torch.randn(B * S, H, D, generator=g, device=dev).to(dt)
+        v = torch.randn(B * S, H, D, generator=g, device=dev).to(dt)
         cu = torch.arange(0, (B + 1) * S, S, dtype=torch.int32, device=dev)
         scale = D ** -0.5 * scale_mul
         out, lse = hip.fwd(q, k, v, cu, cu, S, S, 0.0, scale, False, causal, False, None)[:2]
@@ -38,7 +41,7 @@ def main():
         ref_o = torch.matmul(torch.softmax(s, -1), vd).transpose(1, 2)    # B S H D
         el = lse[:, :, :S].double() - ref_lse
         eo = out.double().view(B, S, H, D) - ref_o
-        print(json.dumps({"lib": a.tag, "B": B, "H": H, "S": S, "D": D, "causal": causal, "scale_mul": scale_mul,
+        print(json.dumps({"lib": a.tag, "dtype": a.dtype, "B": B, "H": H, "S": S, "D": D, "causal": causal, "scale_mul": scale_mul,
                           "lse_mean": float(el.mean()), "lse_maxabs": float(el.abs().max()),
                           "o_mean": float(eo.mean()), "o_maxabs": float(eo.abs().max()),
                           "o_rms": float(eo.pow(2).mean().sqrt())}), flush=True)
