@@ -326,3 +326,15 @@ def test_simulator_catches_a_missing_wait_state():
 def test_asm_forward_d96_in_simulator(lens_q, lens_k, H, D, grid, causal):
     """The D = 96 tile (D = 128 layout, 6 k-steps and 3 d-blocks) at head_dim 96 and 80."""
     _run(lens_q, lens_k, H, D, "bf16", causal=causal, grid=grid, hd=96)
+
+
+def test_simulator_catches_a_wave_dependent_barrier():
+    """A barrier that one wave skips (a wave-dependent branch around it) desynchronises the hardware's
+    barrier counting; the simulator counts each wave's barriers and raises HazardError."""
+    txt = _kernel("bf16")
+    lines = txt.split("\n")
+    i = next(k for k, ln in enumerate(lines) if ln.strip() == "s_barrier")
+    bad = "\n".join(lines[:i] + [f"\ts_cmp_eq_u32 s{gen_fwd.S_WAVE}, 0", "\ts_cbranch_scc1 .Lskipbar_t",
+                                 lines[i], ".Lskipbar_t:"] + lines[i + 1:])
+    with pytest.raises(asm_sim.HazardError):
+        _run_text(bad, [130], [200], 1, 64, "bf16")

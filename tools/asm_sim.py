@@ -267,6 +267,7 @@ class Sim:
             w.s[0] = karg & 0xFFFFFFFF
             w.s[1] = karg >> 32
         steps = 0
+        nbar = [0] * len(waves)
         while not all(w.done for w in waves):
             for w in waves:
                 while not w.done:
@@ -277,8 +278,13 @@ class Sim:
                         raise RuntimeError('step limit')
                     self.count[op] = self.count.get(op, 0) + 1
                     if op == 's_barrier':
+                        nbar[w.id] += 1
                         break
                     self.exec(w, op, args)
+        # every wave of the workgroup must pass the same number of barriers (a wave-dependent branch
+        # around a barrier desynchronises the hardware's barrier counting)
+        if len(set(nbar)) != 1:
+            raise HazardError(f'workgroup {wg}: waves passed different numbers of barriers {nbar}')
 
     # ---------------------------------------------------------------- semantics
     # ---------------------------------------------------------------- completion queues / hazards
