@@ -508,6 +508,90 @@ struct FlashAttnRotaryQKVFn : public torch::autograd::Function<FlashAttnRotaryQK
     }
 };
 
+// ---- bert_padding row moves (flash_attn/bert_padding.py: index_first_axis / index_put_first_axis,
+// the reference's flash_attn/bert_padding.py:11-64). The rows of x are made addressable as row_stride-spaced
+// runs of row_bytes (the inner dimensions contiguous, rows neither overlapping nor broadcast), as
+// bert_padding._rows does, else x is copied out first.
+at::Tensor padding_rows(const at::Tensor &x, int64_t &row_stride, int64_t &row_bytes) {
+    TORCH_CHECK(x.dim() >= 2, "row moves need at least 2 dimensions");
+    int64_t want = 1, row_elems = 1;
+    bool ok = true;
+    for (int64_t d = x.dim() - 1; d >= 1; --d) {
+        if (ok && x.size(d) != 1 && x.stride(d) != want) ok = false;
+        want *= x.size(d);
+        row_elems *= x.size(d);
+    }
+    if (ok && x.size(0) > 1 && x.stride(0) < row_elems) ok = false;
+    at::Tensor y = ok ? x : x.contiguous();
+    const int64_t es = y.element_size();
+    row_stride = y.size(0) > 1 ? y.stride(0) * es : row_elems * es;
+    row_bytes = row_elems * es;
+    return y;
+}
+
+at::Tensor padding_index(const at::Tensor &indices, const at::Tensor &x) {
+    TORCH_CHECK(indices.dim() == 1, "indices must be 1-D");
+    TORCH_CHECK(indices.device() == x.device(), "indices must be on the tensor's device");
+    return (indices.scalar_type() == at::kLong ? indices : indices.to(at::kLong)).contiguous();
+}
+
+// out[i] = src[indices[i]] along dim 0
+at::Tensor gather_rows(const at::Tensor &src_in, const at::Tensor &indices) {
+    c10::DeviceGuard guard(src_in.device());
+    int64_t ss = 0, rb = 0;
+    at::Tensor src = padding_rows(src_in, ss, rb);
+    at::Tensor idx = padding_index(indices, src);
+    std::vector<int64_t> sizes = src.sizes().vec();
+    sizes[0] = idx.size(0);
+    at::Tensor out = at::empty(sizes, src.options());
+    if (out.numel() == 0) return out;
+    const int rc = fa_index_first_axis(src.data_ptr(), src.size(0), ss, idx.data_ptr<int64_t>(), idx.size(0),
+                                       out.data_ptr(), rb, rb, current_stream(src.device()));
+    if (rc != 0) raise_rc(rc, "fa_index_first_axis");
+    return out;
+}
+
+// out = zeros(first_axis_dim, ...); out[indices[i]] = values[i]
+at::Tensor pad_rows(const at::Tensor &values_in, const at::Tensor &indices, int64_t first_axis_dim) {
+    c10::DeviceGuard guard(values_in.device());
+    int64_t vs = 0, rb = 0;
+    at::Tensor values = padding_rows(values_in, vs, rb);
+    at::Tensor idx = padding_index(indices, values);
+    std::vector<int64_t> sizes = values.sizes().vec();
+    sizes[0] = first_axis_dim;
+    at::Tensor out = at::empty(sizes, values.options());
+    if (out.numel() == 0) return out;
+    at::Tensor ws = at::empty({first_axis_dim}, values.options().dtype(at::kInt));
+    const int rc = fa_index_put_first_axis(values.data_ptr(), vs, idx.data_ptr<int64_t>(), idx.size(0), out.data_ptr(),
+                                           first_axis_dim, rb, rb, ws.data_ptr<int32_t>(), current_stream(values.device()));
+    if (rc != 0) raise_rc(rc, "fa_index_put_first_axis");
+    return out;
+}
+
+struct IndexFirstAxisFn : public torch::autograd::Function<IndexFirstAxisFn> {
+    static variable_list forward(AutogradContext *ctx, const at::Tensor &input, const at::Tensor &indices) {
+        ctx->save_for_backward({indices});
+        ctx->saved_data["n"] = input.size(0);
+        return {gather_rows(input, indices)};
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list g) {
+        auto t = ctx->get_saved_variables();
+        return {pad_rows(g[0], t[0], ctx->saved_data["n"].toInt()), at::Tensor()};
+    }
+};
+
+struct IndexPutFirstAxisFn : public torch::autograd::Function<IndexPutFirstAxisFn> {
+    static variable_list forward(AutogradContext *ctx, const at::Tensor &values, const at::Tensor &indices,
+                                 int64_t first_axis_dim) {
+        ctx->save_for_backward({indices});
+        return {pad_rows(values, indices, first_axis_dim)};
+    }
+    static variable_list backward(AutogradContext *ctx, variable_list g) {
+        auto t = ctx->get_saved_variables();
+        return {gather_rows(g[0], t[0]), at::Tensor(), at::Tensor()};
+    }
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_fa_C, m) {
@@ -556,5 +640,15 @@ PYBIND11_MODULE(_fa_C, m) {
              int64_t impl) {
               return FlashAttnRotaryQKVFn::apply(qkv, cos, sin, cu, p, scale, causal, seed, offset, od, impl)[0];
           });
+    m.def("index_first_axis", [](const at::Tensor &input, const at::Tensor &indices) {
+        TORCH_CHECK(input.dim() >= 2, "index_first_axis: input must have at least 2 dimensions");
+        if (!needs_grad({&input})) return gather_rows(input, indices);
+        return IndexFirstAxisFn::apply(input, indices)[0];
+    });
+    m.def("index_put_first_axis", [](const at::Tensor &values, const at::Tensor &indices, int64_t first_axis_dim) {
+        TORCH_CHECK(indices.dim() == 1 && values.dim() >= 2, "index_put_first_axis: 1-D indices, values of 2+ dims");
+        if (!needs_grad({&values})) return pad_rows(values, indices, first_axis_dim);
+        return IndexPutFirstAxisFn::apply(values, indices, first_axis_dim)[0];
+    });
     m.def("version", [] { return std::string(fa_version()); });
 }

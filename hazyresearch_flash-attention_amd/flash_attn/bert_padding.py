@@ -7,7 +7,11 @@ first axis.
 
 On GPU tensors the row moves run in HIP (libfa_hip.so: fa_index_first_axis,
 fa_index_put_first_axis, fa_index_add_first_axis; csrc/fa_padding.hip), which raise if the
-library is missing. Host tensors use torch indexing, as the reference does on any device.
+library is missing. index_first_axis and index_put_first_axis go through the compiled binding
+(_fa_C: checks, allocation, launch and the autograd node in C++; the ctypes path below cost about
+twice the kernel's time per call on the host) when it is loaded; the autograd functions below
+are the same operations over ctypes. Host tensors use torch indexing, as the reference does on any
+device.
 """
 import ctypes
 
@@ -133,7 +137,17 @@ class IndexFirstAxis(torch.autograd.Function):
         return _pad(grad_output, indices, ctx.first_axis_dim), None
 
 
-index_first_axis = IndexFirstAxis.apply
+def _compiled():
+    from flash_attn import flash_attn_hip
+    return flash_attn_hip._C
+
+
+def index_first_axis(input, indices):
+    """input[indices] along dim 0 (IndexFirstAxis, reference :11-38); CUDA tensors through _fa_C."""
+    C = _compiled()
+    if C is not None and input.is_cuda:
+        return C.index_first_axis(input, indices)
+    return IndexFirstAxis.apply(input, indices)
 
 
 class IndexPutFirstAxis(torch.autograd.Function):
@@ -151,7 +165,13 @@ class IndexPutFirstAxis(torch.autograd.Function):
         return _gather(grad_output, indices), None, None
 
 
-index_put_first_axis = IndexPutFirstAxis.apply
+def index_put_first_axis(values, indices, first_axis_dim):
+    """zeros(first_axis_dim, ...) with rows `indices` = values (IndexPutFirstAxis, reference :41-64);
+    CUDA tensors through _fa_C."""
+    C = _compiled()
+    if C is not None and values.is_cuda:
+        return C.index_put_first_axis(values, indices, first_axis_dim)
+    return IndexPutFirstAxis.apply(values, indices, first_axis_dim)
 
 
 class IndexFirstAxisResidual(torch.autograd.Function):

@@ -85,3 +85,33 @@ def test_index_first_axis_residual(dtype):
     ref.index_add_(0, idx, go)
     (gx,) = torch.autograd.grad((out, res), (x,), (go, gr))
     assert torch.equal(gx, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+def test_compiled_and_ctypes_routes_agree(dtype):
+    """index_first_axis / index_put_first_axis take the compiled binding (_fa_C) on CUDA tensors; the
+    ctypes autograd functions (IndexFirstAxis / IndexPutFirstAxis) are the same operations: bitwise
+    equal outputs and gradients, strided sources included."""
+    bp = _bp()
+    from flash_attn import flash_attn_hip as hip
+    if hip._C is None:
+        pytest.skip("compiled binding not loaded (FA_HIP_LIB variant)")
+    g = torch.Generator().manual_seed(7)
+    base = torch.randn(400, 2, 6, 16, generator=g).to(dtype).to(DEV)
+    src = base[:, 1]                                           # strided rows
+    idx = torch.randperm(400, generator=g)[:257].to(DEV)
+    assert torch.equal(bp.index_first_axis(src, idx), bp.IndexFirstAxis.apply(src, idx))
+    vals = torch.randn(257, 6, 16, generator=g).to(dtype).to(DEV)
+    assert torch.equal(bp.index_put_first_axis(vals, idx, 400), bp.IndexPutFirstAxis.apply(vals, idx, 400))
+    x = src.detach().clone().requires_grad_()
+    go = torch.randn(257, 6, 16, generator=g).to(dtype).to(DEV)
+    (g_c,) = torch.autograd.grad(bp.index_first_axis(x, idx), (x,), go)
+    (g_p,) = torch.autograd.grad(bp.IndexFirstAxis.apply(x, idx), (x,), go)
+    assert torch.equal(g_c, g_p)
+    v = vals.clone().requires_grad_()
+    gp = torch.randn(400, 6, 16, generator=g).to(dtype).to(DEV)
+    (gv_c,) = torch.autograd.grad(bp.index_put_first_axis(v, idx, 400), (v,), gp)
+    (gv_p,) = torch.autograd.grad(bp.IndexPutFirstAxis.apply(v, idx, 400), (v,), gp)
+    assert torch.equal(gv_c, gv_p)
+    with pytest.raises(RuntimeError):
+        bp.index_first_axis(src, idx.cpu())                    # indices on another device
