@@ -541,6 +541,7 @@ at::Tensor gather_rows(const at::Tensor &src_in, const at::Tensor &indices) {
     int64_t ss = 0, rb = 0;
     at::Tensor src = padding_rows(src_in, ss, rb);
     at::Tensor idx = padding_index(indices, src);
+    if (rb % 2) return src.index_select(0, idx);     // odd-byte rows (1-byte dtypes): the C ABI moves 2-byte words
     std::vector<int64_t> sizes = src.sizes().vec();
     sizes[0] = idx.size(0);
     at::Tensor out = at::empty(sizes, src.options());
@@ -559,6 +560,7 @@ at::Tensor pad_rows(const at::Tensor &values_in, const at::Tensor &indices, int6
     at::Tensor idx = padding_index(indices, values);
     std::vector<int64_t> sizes = values.sizes().vec();
     sizes[0] = first_axis_dim;
+    if (rb % 2) return at::zeros(sizes, values.options()).index_copy_(0, idx, values);   // odd-byte rows
     at::Tensor out = at::empty(sizes, values.options());
     if (out.numel() == 0) return out;
     at::Tensor ws = at::empty({first_axis_dim}, values.options().dtype(at::kInt));

@@ -61,6 +61,8 @@ def _gather(src, indices):
     hip = _hip()
     src, sstride, row_bytes = _rows(src)
     indices = _idx64(indices).contiguous()
+    if row_bytes % 2:      # odd-byte rows (1-byte dtypes): the C ABI moves 2-byte words
+        return src.index_select(0, indices)
     out = torch.empty((indices.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
     if out.numel() == 0:
         return out
@@ -83,6 +85,9 @@ def _pad(values, indices, first_axis_dim):
     hip = _hip()
     values, vstride, row_bytes = _rows(values)
     indices = _idx64(indices).contiguous()
+    if row_bytes % 2:      # odd-byte rows (1-byte dtypes)
+        out = values.new_zeros((first_axis_dim,) + tuple(values.shape[1:]))
+        return out.index_copy_(0, indices, values)
     out = torch.empty((first_axis_dim,) + tuple(values.shape[1:]), dtype=values.dtype, device=values.device)
     if out.numel() == 0:
         return out

@@ -115,3 +115,16 @@ def test_compiled_and_ctypes_routes_agree(dtype):
     assert torch.equal(gv_c, gv_p)
     with pytest.raises(RuntimeError):
         bp.index_first_axis(src, idx.cpu())                    # indices on another device
+
+
+def test_odd_byte_rows():
+    """1-byte dtypes with an odd row size (the C ABI moves 2-byte words) keep the reference's torch
+    indexing semantics on the device."""
+    bp = _bp()
+    x = torch.randint(0, 255, (50, 3), dtype=torch.uint8, device=DEV)
+    idx = torch.randperm(50, device=DEV)[:17]
+    assert torch.equal(bp.index_first_axis(x, idx), x[idx])
+    ref = torch.zeros(50, 3, dtype=torch.uint8, device=DEV)
+    ref[idx] = x[:17]
+    assert torch.equal(bp.index_put_first_axis(x[:17], idx, 50), ref)
+    assert torch.equal(bp.IndexFirstAxis.apply(x, idx), x[idx])
